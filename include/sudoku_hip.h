@@ -1,0 +1,93 @@
+/*
+ * sudoku_hip.h -- C ABI of the MI355X (gfx950) Sudoku solver library
+ * (libsudoku_hip.so, built from sudoku_solver_distributed_amd/csrc/).
+ *
+ * Plain pointers and sizes only.  Every `d_*` pointer is DEVICE memory on the
+ * calling thread's current HIP device; `stream` is a hipStream_t (NULL = the
+ * default stream).  Calls are asynchronous on `stream` unless noted.
+ *
+ * Grid format: 81 bytes per board, row-major, 0 = empty, 1..9 = digit; a batch
+ * of n boards is n*81 contiguous bytes.
+ *
+ * Return codes: 0 = launched / ok, <0 = error (text in sdk_last_error()).
+ *
+ * Each entry point replaces one reference interface
+ * (cristiano-nicolau/sudoku_solver_distributed):
+ */
+#ifndef SUDOKU_HIP_H
+#define SUDOKU_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* per-board status written by the solvers */
+#define SDK_UNSOLVABLE 0  /* gen.py:28 `return False`; output = input board   */
+#define SDK_SOLVED 1      /* gen.py:18/25 `return True`; output = filled board */
+#define SDK_INVALID -1    /* a byte > 9 in the input (rejected, output = input) */
+#define SDK_CANCELLED -2  /* ordered mode: a lower-indexed board already solved */
+
+/* Bytes of device workspace sdk_solve_batch needs (queue heads, cancel word,
+ * statistics).  Allocate once, zero once; the library re-arms the per-call
+ * words itself with a hipMemsetAsync on `stream`. */
+size_t sdk_workspace_bytes(void);
+
+/* Solve n boards.  For every board the output is the FIRST solution of the
+ * reference's backtracking walk -- first empty cell in row-major order,
+ * digits 1..9 ascending -- i.e. bit-identical to
+ *   gen.py:6-28        solve_sudoku(board)
+ *   node.py:31-40,62-74 SudokuSolver.solve_sudoku / solve_sudoku_recursive
+ * (node.py differs only on boards whose givens already clash).
+ * d_puzzles and d_solutions may alias.  `ordered` != 0 selects frontier mode:
+ * once board i is solved, boards j > i are abandoned (status SDK_CANCELLED)
+ * and the lowest solved index is kept in the workspace (sdk_read_stats).  */
+int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status,
+                    int64_t n, void *d_workspace, int ordered, void *stream);
+
+/* Batch Sudoku.check (mode 0, sudoku.py:119-140: every row, column and box
+ * sums to 45 and holds 9 distinct values) or node.py's SudokuSolver.check
+ * (mode 1, node.py:82-116: sums only).  d_ok[i] = 1/0. */
+int sdk_check_batch(const uint8_t *d_grids, int32_t *d_ok, int64_t n, int mode, void *stream);
+
+/* Batch of node.py "solve" tasks (node.py:384-406 -> 76-80,
+ * SudokuSolver.solve_sudoku_destributed): d_num[i] = first digit 1..9 that
+ * is_valid_move (node.py:42-60) accepts at cell d_cells[i] (= row*9+col) of
+ * board i, or 0 for None. */
+int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
+                              int32_t *d_num, int64_t n, void *stream);
+
+/* One level of the reference walk's search tree, for splitting a single hard
+ * board over waves / GPUs (node.py's per-cell peer task split, node.py:419-449,
+ * re-designed as a frontier split).  Every input node is propagated; then
+ *   dead   -> no child,
+ *   solved -> one child: the solved grid,
+ *   open   -> one child per candidate of its first empty cell (row-major),
+ *             digits ascending.
+ * Children of all nodes, concatenated in input order, are therefore in the
+ * walk's (lexicographic) order, and the first SOLVED child of the frontier
+ * carries the walk's first solution.
+ *   d_tmp:      scratch, n*81 bytes
+ *   d_offsets:  n+1 int64; d_offsets[n] = total children (read it back)
+ *   d_children: capacity cap*81 bytes; children past cap are not written.
+ * Caller checks d_offsets[n] <= cap. */
+int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64_t *d_offsets,
+                        uint8_t *d_children, int64_t cap, void *stream);
+
+/* Copy statistics to host (synchronous on `stream`):
+ * out[0] boards finished, out[1] boards solved, out[2] guesses (DFS nodes),
+ * out[3] propagation sweeps, out[4] lowest solved index in ordered mode
+ * (INT64_MAX if none), out[5] reserved.  reset != 0 zeroes them afterwards. */
+int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
+
+/* Library / device info. */
+const char *sdk_last_error(void);
+const char *sdk_version(void);
+int sdk_device_cu_count(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SUDOKU_HIP_H */

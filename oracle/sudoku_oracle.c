@@ -1,0 +1,352 @@
+/*
+ * sudoku_oracle.c -- CPU restatement of the reference's Sudoku algorithms.
+ *
+ * TEST INFRASTRUCTURE ONLY.  This file is the parity checker for the HIP
+ * solver in sudoku_solver_distributed_amd/csrc.  Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it; the product path never does.
+ *
+ * Parity pinning: the restatement is checked against golden vectors produced
+ * by importing the reference's own gen.py / sudoku.py / node.py
+ * (tests/golden/make_golden.py writes the JSON fixtures, see tests/test_oracle.py).
+ *
+ * Grid layout everywhere: 81 bytes, row-major, 0 = empty, 1..9 = digit.
+ *
+ * Reference functions restated (cristiano-nicolau/sudoku_solver_distributed):
+ *   oracle_is_valid        <- sudoku.py:60-78   Sudoku.check_is_valid
+ *   oracle_check           <- sudoku.py:80-140  Sudoku.check_row/column/square/check
+ *   oracle_check_sums      <- node.py:82-116    SudokuSolver.check (sums only)
+ *   oracle_is_valid_move   <- node.py:42-60     SudokuSolver.is_valid_move
+ *   oracle_solve           <- gen.py:6-28       solve_sudoku (row-major, 1..9)
+ *   oracle_solve_node      <- node.py:62-74     SudokuSolver.solve_sudoku_recursive
+ *   oracle_first_candidate <- node.py:76-80     SudokuSolver.solve_sudoku_destributed
+ *   oracle_count_solutions    (test helper: uniqueness of generated puzzles)
+ */
+#include <stdint.h>
+#include <string.h>
+
+/* sudoku.py:60-78 -- num not in row, not in column, not in 3x3 box. */
+int oracle_is_valid(const uint8_t *g, int row, int col, int num)
+{
+    for (int i = 0; i < 9; i++)
+        if (g[row * 9 + i] == num || g[i * 9 + col] == num)
+            return 0;
+    int sr = 3 * (row / 3), sc = 3 * (col / 3);
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++)
+            if (g[(sr + i) * 9 + sc + j] == num)
+                return 0;
+    return 1;
+}
+
+/* sudoku.py:85/95-98/108-113: sum(unit) == 45 and len(set(unit)) == 9 */
+static int unit_ok_sum_set(const int *v)
+{
+    int sum = 0;
+    int seen[256];
+    memset(seen, 0, sizeof seen);
+    int distinct = 0;
+    for (int k = 0; k < 9; k++) {
+        sum += v[k];
+        if (!seen[v[k] & 255]) { seen[v[k] & 255] = 1; distinct++; }
+    }
+    return sum == 45 && distinct == 9;
+}
+
+/* sudoku.py:119-140 -- rows, then columns, then squares. */
+int oracle_check(const uint8_t *g)
+{
+    int v[9];
+    for (int r = 0; r < 9; r++) {
+        for (int k = 0; k < 9; k++) v[k] = g[r * 9 + k];
+        if (!unit_ok_sum_set(v)) return 0;
+    }
+    for (int c = 0; c < 9; c++) {
+        for (int k = 0; k < 9; k++) v[k] = g[k * 9 + c];
+        if (!unit_ok_sum_set(v)) return 0;
+    }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            int n = 0;
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) v[n++] = g[(i * 3 + a) * 9 + j * 3 + b];
+            if (!unit_ok_sum_set(v)) return 0;
+        }
+    return 1;
+}
+
+/* node.py:82-116 -- only the sums are checked (no distinctness). */
+int oracle_check_sums(const uint8_t *g)
+{
+    for (int r = 0; r < 9; r++) {
+        int s = 0;
+        for (int k = 0; k < 9; k++) s += g[r * 9 + k];
+        if (s != 45) return 0;
+    }
+    for (int c = 0; c < 9; c++) {
+        int s = 0;
+        for (int k = 0; k < 9; k++) s += g[k * 9 + c];
+        if (s != 45) return 0;
+    }
+    for (int i = 0; i < 3; i++)
+        for (int j = 0; j < 3; j++) {
+            int s = 0;
+            for (int a = 0; a < 3; a++)
+                for (int b = 0; b < 3; b++) s += g[(i * 3 + a) * 9 + j * 3 + b];
+            if (s != 45) return 0;
+        }
+    return 1;
+}
+
+/* node.py:42-60 -- is_valid_move short-circuits to True when check() passes,
+ * then scans row+column together, then the box. */
+int oracle_is_valid_move(const uint8_t *g, int row, int col, int num)
+{
+    if (oracle_check_sums(g)) return 1;
+    return oracle_is_valid(g, row, col, num);
+}
+
+typedef int (*valid_fn)(const uint8_t *, int, int, int);
+
+static uint64_t g_nodes; /* candidate tests (the reference's "validations") */
+
+/* gen.py:6-28 -- first empty cell in row-major order, digits 1..9 ascending,
+ * recursion; the board is restored to its input on failure. */
+static int solve_rec(uint8_t *g, valid_fn valid)
+{
+    int cell = -1;
+    for (int i = 0; i < 81; i++)
+        if (g[i] == 0) { cell = i; break; }
+    if (cell < 0) return 1;
+    int row = cell / 9, col = cell % 9;
+    for (int num = 1; num <= 9; num++) {
+        g_nodes++;
+        if (valid(g, row, col, num)) {
+            g[cell] = (uint8_t)num;
+            if (solve_rec(g, valid)) return 1;
+            g[cell] = 0;
+        }
+    }
+    return 0;
+}
+
+int oracle_solve(uint8_t *g)
+{
+    return solve_rec(g, oracle_is_valid);
+}
+
+/* node.py:62-74 (same walk, node.py's is_valid_move as the test). */
+int oracle_solve_node(uint8_t *g)
+{
+    return solve_rec(g, oracle_is_valid_move);
+}
+
+uint64_t oracle_last_nodes(void) { return g_nodes; }
+void oracle_reset_nodes(void) { g_nodes = 0; }
+
+/* node.py:76-80 -- first digit 1..9 accepted by is_valid_move, or 0 (None). */
+int oracle_first_candidate(const uint8_t *g, int row, int col)
+{
+    for (int num = 1; num <= 9; num++)
+        if (oracle_is_valid_move(g, row, col, num)) return num;
+    return 0;
+}
+
+/* Batch form of oracle_solve: in -> out (81 B each), status 1 = solved,
+ * 0 = no solution (out = input, as gen.py leaves the board). */
+void oracle_solve_batch(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n)
+{
+    for (int64_t p = 0; p < n; p++) {
+        memcpy(out + p * 81, in + p * 81, 81);
+        status[p] = oracle_solve(out + p * 81);
+    }
+}
+
+/* Test helper: number of completions (up to `limit`) under the reference's
+ * constraint (every empty cell differs from its filled peers). */
+static int count_rec(uint8_t *g, int limit, int *count)
+{
+    int cell = -1;
+    for (int i = 0; i < 81; i++)
+        if (g[i] == 0) { cell = i; break; }
+    if (cell < 0) { (*count)++; return *count >= limit; }
+    int row = cell / 9, col = cell % 9;
+    for (int num = 1; num <= 9; num++) {
+        if (oracle_is_valid(g, row, col, num)) {
+            g[cell] = (uint8_t)num;
+            int stop = count_rec(g, limit, count);
+            g[cell] = 0;
+            if (stop) return 1;
+        }
+    }
+    return 0;
+}
+
+int oracle_count_solutions(const uint8_t *g_in, int limit)
+{
+    uint8_t g[81];
+    memcpy(g, g_in, 81);
+    int count = 0;
+    count_rec(g, limit, &count);
+    return count;
+}
+
+/* Test helper: the same count with row/col/box bitmasks and
+ * fewest-candidates branching -- used only to certify that generated
+ * benchmark puzzles have a unique solution (order does not matter for a
+ * count).  Same constraint as count_rec. */
+static int fast_rec(uint8_t *g, uint16_t *rm, uint16_t *cm, uint16_t *bm,
+                    int limit, int *count)
+{
+    int best = -1, bestn = 10;
+    uint16_t bestc = 0;
+    for (int i = 0; i < 81; i++) {
+        if (g[i]) continue;
+        int r = i / 9, c = i % 9, b = (r / 3) * 3 + c / 3;
+        uint16_t cand = (uint16_t)(~(rm[r] | cm[c] | bm[b]) & 0x1FF);
+        int n = __builtin_popcount(cand);
+        if (n < bestn) { bestn = n; best = i; bestc = cand; if (n <= 1) break; }
+    }
+    if (best < 0) { (*count)++; return *count >= limit; }
+    if (bestn == 0) return 0;
+    int r = best / 9, c = best % 9, b = (r / 3) * 3 + c / 3;
+    while (bestc) {
+        int d = __builtin_ctz(bestc);
+        bestc &= (uint16_t)(bestc - 1);
+        uint16_t bit = (uint16_t)(1u << d);
+        g[best] = (uint8_t)(d + 1);
+        rm[r] |= bit; cm[c] |= bit; bm[b] |= bit;
+        int stop = fast_rec(g, rm, cm, bm, limit, count);
+        rm[r] &= (uint16_t)~bit; cm[c] &= (uint16_t)~bit; bm[b] &= (uint16_t)~bit;
+        g[best] = 0;
+        if (stop) return 1;
+    }
+    return 0;
+}
+
+int oracle_count_solutions_fast(const uint8_t *g_in, int limit)
+{
+    uint8_t g[81];
+    uint16_t rm[9] = {0}, cm[9] = {0}, bm[9] = {0};
+    memcpy(g, g_in, 81);
+    for (int i = 0; i < 81; i++) {
+        if (!g[i]) continue;
+        int r = i / 9, c = i % 9, b = (r / 3) * 3 + c / 3;
+        uint16_t bit = (uint16_t)(1u << (g[i] - 1));
+        /* a duplicated given makes the reference's walk ignore the clash
+         * (only empty cells are tested), so record it without failing */
+        rm[r] |= bit; cm[c] |= bit; bm[b] |= bit;
+    }
+    int count = 0;
+    fast_rec(g, rm, cm, bm, limit, &count);
+    return count;
+}
+
+/* Test helper: fewest-candidates search that also returns the first
+ * completion it meets and whether it is the only one (count up to 2).  For a
+ * board with exactly one completion that completion is, necessarily, the
+ * walk's (gen.py:6-28) answer -- lets tests pin hard 17-clue boards at
+ * scale, where the literal walk needs up to ~1e9 candidate tests. */
+static int uniq_rec(uint8_t *g, uint16_t *rm, uint16_t *cm, uint16_t *bm,
+                    int *count, uint8_t *first)
+{
+    int best = -1, bestn = 10;
+    uint16_t bestc = 0;
+    for (int i = 0; i < 81; i++) {
+        if (g[i]) continue;
+        int r = i / 9, c = i % 9, b = (r / 3) * 3 + c / 3;
+        uint16_t cand = (uint16_t)(~(rm[r] | cm[c] | bm[b]) & 0x1FF);
+        int n = __builtin_popcount(cand);
+        if (n < bestn) { bestn = n; best = i; bestc = cand; if (n <= 1) break; }
+    }
+    if (best < 0) {
+        if (*count == 0) memcpy(first, g, 81);
+        (*count)++;
+        return *count >= 2;
+    }
+    if (bestn == 0) return 0;
+    int r = best / 9, c = best % 9, b = (r / 3) * 3 + c / 3;
+    while (bestc) {
+        int d = __builtin_ctz(bestc);
+        bestc &= (uint16_t)(bestc - 1);
+        uint16_t bit = (uint16_t)(1u << d);
+        g[best] = (uint8_t)(d + 1);
+        rm[r] |= bit; cm[c] |= bit; bm[b] |= bit;
+        int stop = uniq_rec(g, rm, cm, bm, count, first);
+        rm[r] &= (uint16_t)~bit; cm[c] &= (uint16_t)~bit; bm[b] &= (uint16_t)~bit;
+        g[best] = 0;
+        if (stop) return 1;
+    }
+    return 0;
+}
+
+/* returns the number of completions capped at 2; out = first one found */
+int oracle_solve_unique(const uint8_t *g_in, uint8_t *out)
+{
+    uint8_t g[81];
+    uint16_t rm[9] = {0}, cm[9] = {0}, bm[9] = {0};
+    memcpy(g, g_in, 81);
+    memcpy(out, g_in, 81);
+    for (int i = 0; i < 81; i++) {
+        if (!g[i]) continue;
+        int r = i / 9, c = i % 9, b = (r / 3) * 3 + c / 3;
+        uint16_t bit = (uint16_t)(1u << (g[i] - 1));
+        rm[r] |= bit; cm[c] |= bit; bm[b] |= bit;
+    }
+    int count = 0;
+    uniq_rec(g, rm, cm, bm, &count, out);
+    return count;
+}
+
+void oracle_solve_unique_batch(const uint8_t *in, uint8_t *out, int32_t *count, int64_t n)
+{
+    for (int64_t p = 0; p < n; p++) count[p] = oracle_solve_unique(in + p * 81, out + p * 81);
+}
+
+/* Timed batch walk for bench.py's cpu_baseline: solves boards in order until
+ * `seconds` of wall time have elapsed; returns the number of boards fully
+ * solved (a board cut off by the deadline is not counted). */
+#include <time.h>
+static double g_deadline;
+static int g_abort;
+
+static double now_s(void)
+{
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return ts.tv_sec + ts.tv_nsec * 1e-9;
+}
+
+static int solve_rec_timed(uint8_t *g)
+{
+    int cell = -1;
+    for (int i = 0; i < 81; i++)
+        if (g[i] == 0) { cell = i; break; }
+    if (cell < 0) return 1;
+    int row = cell / 9, col = cell % 9;
+    for (int num = 1; num <= 9; num++) {
+        if ((++g_nodes & 0xFFFFF) == 0 && now_s() > g_deadline) g_abort = 1;
+        if (g_abort) return 0;
+        if (oracle_is_valid(g, row, col, num)) {
+            g[cell] = (uint8_t)num;
+            if (solve_rec_timed(g)) return 1;
+            if (g_abort) return 0;
+            g[cell] = 0;
+        }
+    }
+    return 0;
+}
+
+int64_t oracle_solve_batch_timed(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n, double seconds)
+{
+    g_deadline = now_s() + seconds;
+    g_abort = 0;
+    int64_t done = 0;
+    for (int64_t p = 0; p < n; p++) {
+        memcpy(out + p * 81, in + p * 81, 81);
+        status[p] = solve_rec_timed(out + p * 81);
+        if (g_abort) break;
+        done++;
+        if (now_s() > g_deadline) break;
+    }
+    return done;
+}

@@ -1,0 +1,76 @@
+"""ctypes binding of libsudoku_hip.so (the C ABI declared in include/sudoku_hip.h).
+
+There is no fallback: if the library is missing or fails to load, every entry
+point raises.  Build it with ``python -m sudoku_solver_distributed_amd.build``
+(or ``__graft_entry__.build()``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsudoku_hip.so")
+
+SDK_UNSOLVABLE = 0
+SDK_SOLVED = 1
+SDK_INVALID = -1
+SDK_CANCELLED = -2
+
+# every symbol include/sudoku_hip.h declares
+EXPORTS = (
+    "sdk_workspace_bytes",
+    "sdk_solve_batch",
+    "sdk_check_batch",
+    "sdk_first_candidate_batch",
+    "sdk_expand_frontier",
+    "sdk_read_stats",
+    "sdk_last_error",
+    "sdk_version",
+    "sdk_device_cu_count",
+)
+
+_lib = None
+
+
+class SudokuHipError(RuntimeError):
+    pass
+
+
+def load() -> ctypes.CDLL:
+    """Load the HIP library (raises SudokuHipError if it is absent)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise SudokuHipError(
+            f"{LIB_PATH} not found: build it with `python -m sudoku_solver_distributed_amd.build`"
+        )
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i64, i32, sz = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_size_t
+    L.sdk_workspace_bytes.restype = sz
+    L.sdk_workspace_bytes.argtypes = []
+    L.sdk_solve_batch.restype = i32
+    L.sdk_solve_batch.argtypes = [vp, vp, vp, i64, vp, i32, vp]
+    L.sdk_check_batch.restype = i32
+    L.sdk_check_batch.argtypes = [vp, vp, i64, i32, vp]
+    L.sdk_first_candidate_batch.restype = i32
+    L.sdk_first_candidate_batch.argtypes = [vp, vp, vp, i64, vp]
+    L.sdk_expand_frontier.restype = i32
+    L.sdk_expand_frontier.argtypes = [vp, i64, vp, vp, vp, i64, vp]
+    L.sdk_read_stats.restype = i32
+    L.sdk_read_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i32, vp]
+    L.sdk_last_error.restype = ctypes.c_char_p
+    L.sdk_last_error.argtypes = []
+    L.sdk_version.restype = ctypes.c_char_p
+    L.sdk_version.argtypes = []
+    L.sdk_device_cu_count.restype = i32
+    L.sdk_device_cu_count.argtypes = []
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = load().sdk_last_error().decode(errors="replace")
+        raise SudokuHipError(f"{what} failed ({rc}): {msg}")

@@ -1,0 +1,40 @@
+"""Build libsudoku_hip.so in-tree for gfx950 with hipcc (no JIT, no torch ext).
+
+    python -m sudoku_solver_distributed_amd.build
+"""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(_HERE)
+SRC = os.path.join(_HERE, "csrc", "sudoku_kernels.hip")
+OUT = os.path.join(_HERE, "libsudoku_hip.so")
+ARCH = os.environ.get("SDK_OFFLOAD_ARCH", "gfx950")
+
+
+def hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    return "hipcc"
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    deps = [SRC, os.path.join(ROOT, "include", "sudoku_hip.h")]
+    if (not force and os.path.exists(OUT)
+            and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
+        return OUT
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
+           "-Wall", "-o", OUT + ".tmp", SRC]
+    if verbose:
+        cmd.append("-Rpass-analysis=kernel-resource-usage")
+    subprocess.check_call(cmd)
+    os.replace(OUT + ".tmp", OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))

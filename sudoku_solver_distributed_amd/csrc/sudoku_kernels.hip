@@ -1,0 +1,700 @@
+// sudoku_kernels.hip -- MI355X (gfx950, CDNA4) Sudoku solver kernels + C ABI.
+//
+// Hot path: batch solving of 9x9 boards, bit-identical to the reference's
+// backtracking walk (gen.py:6-28 solve_sudoku; node.py:62-74
+// SudokuSolver.solve_sudoku_recursive): the walk fills the FIRST empty cell in
+// row-major order with digits 1..9 ascending, so its first solution is the
+// lexicographically smallest completion.  We reach the same board with far
+// fewer nodes by interleaving sound propagation (naked singles, hidden
+// singles, conflict detection) with branching on that same first empty cell
+// in the same digit order: propagation only removes completions, never
+// reorders them, so the first completion found is still the smallest one.
+//
+// Execution model:
+//   * one 64-lane wavefront owns one board; lane l owns cell l (slot 0) and,
+//     for l < 17, cell 64+l (slot 1);
+//   * the 27 unit masks (rows 0-8, columns 9-17, boxes 18-26; bit d-1 = digit
+//     d used) are rebuilt every sweep in the wave's LDS slice with ds_or
+//     atomics, which also detect two placements of one digit in one unit;
+//   * hidden singles come from per-unit "seen once" / "seen twice" masks built
+//     with returning ds_or atomics (old & cand = second sighting);
+//   * backtracking is a trail: every cell remembers the depth at which it was
+//     filled, so undoing a guess is one compare per lane; the DFS stack (cell,
+//     untried digits) is 16 bits per level, kept one level per lane in two
+//     VGPRs and read/written with readlane / lane-select;
+//   * waves are persistent and pull boards from a chunked global queue.
+// No MFMA: this is branchy 9-bit mask work, VALU + LDS bound.
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string.h>
+#include <stdio.h>
+#include <atomic>
+#include <mutex>
+
+#include "../../include/sudoku_hip.h"
+
+#define WAVES_PER_BLOCK 4
+#define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
+
+// ---------------------------------------------------------------- workspace
+// word layout of the device workspace (uint64 words)
+enum {
+    WS_QUEUE = 0,      // chunked board queue head (re-armed every call)
+    WS_BEST = 1,       // ordered mode: lowest solved index (re-armed to INT64_MAX)
+    WS_ARM_WORDS = 2,  // words re-armed per call
+    WS_FINISHED = 8,   // statistics (accumulate until sdk_read_stats(reset))
+    WS_SOLVED = 9,
+    WS_GUESSES = 10,
+    WS_SWEEPS = 11,
+    WS_WORDS = 16
+};
+
+struct __attribute__((aligned(16))) WaveLds {
+    uint32_t M[28];  // unit masks of filled cells
+    uint32_t O[28];  // digits seen at least once among empty cells' candidates
+    uint32_t T[28];  // digits seen at least twice
+    uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
+    uint32_t pad[3];
+};
+
+__device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
+
+// Orders this wave's LDS accesses (a single wave's DS ops execute in order;
+// this keeps the compiler from moving them and drains returns).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Per-lane view of its two cells.
+struct Cells {
+    uint32_t v0, v1;    // digit 0..9 (0 = empty)
+    uint32_t lv0, lv1;  // depth at which the cell was filled (givens: 0)
+    bool g0, g1;        // given
+    int r0, c0, b0, r1, c1, b1;
+    bool has1;
+};
+
+__device__ __forceinline__ void cell_units(int cell, int &r, int &c, int &b)
+{
+    r = cell / 9;
+    c = cell - r * 9;
+    b = (r / 3) * 3 + c / 3;
+}
+
+// Load one board (81 bytes) into the wave.  Returns false (wave-uniform) if
+// any byte is > 9.
+__device__ __forceinline__ bool load_board(const uint8_t *__restrict__ src, int lane, Cells &s)
+{
+    s.has1 = lane < 17;
+    uint32_t a = src[lane];
+    uint32_t b = s.has1 ? (uint32_t)src[64 + lane] : 0u;
+    s.v0 = a;
+    s.v1 = b;
+    s.g0 = a != 0;
+    s.g1 = s.has1 && b != 0;
+    s.lv0 = 0;
+    s.lv1 = 0;
+    return !__any(a > 9 || b > 9);
+}
+
+// Build the givens' unit masks (returned in lanes 0..26) and the bad-unit mask.
+__device__ __forceinline__ uint32_t build_given_masks(WaveLds &W, int lane, const Cells &s, uint32_t &bad)
+{
+    if (lane < 28) W.M[lane] = 0;
+    if (lane == 0) W.bad = 0;
+    wave_lds_sync();
+    if (s.g0) {
+        uint32_t bit = 1u << (s.v0 - 1);
+        uint32_t d = 0;
+        if (atomicOr(&W.M[s.r0], bit) & bit) d |= 1u << s.r0;
+        if (atomicOr(&W.M[9 + s.c0], bit) & bit) d |= 1u << (9 + s.c0);
+        if (atomicOr(&W.M[18 + s.b0], bit) & bit) d |= 1u << (18 + s.b0);
+        if (d) atomicOr(&W.bad, d);
+    }
+    if (s.g1) {
+        uint32_t bit = 1u << (s.v1 - 1);
+        uint32_t d = 0;
+        if (atomicOr(&W.M[s.r1], bit) & bit) d |= 1u << s.r1;
+        if (atomicOr(&W.M[9 + s.c1], bit) & bit) d |= 1u << (9 + s.c1);
+        if (atomicOr(&W.M[18 + s.b1], bit) & bit) d |= 1u << (18 + s.b1);
+        if (d) atomicOr(&W.bad, d);
+    }
+    wave_lds_sync();
+    bad = __builtin_amdgcn_readfirstlane(W.bad);
+    return lane < 27 ? W.M[lane] : 0u;
+}
+
+enum { PROP_OPEN = 0, PROP_DEAD = 1, PROP_SOLVED = 2 };
+
+// One propagation sweep.  Returns PROP_DEAD on a contradiction, PROP_SOLVED
+// when no cell is empty, otherwise PROP_OPEN and sets `placed` if any single
+// was placed (then call again).  When it returns PROP_OPEN with !placed the
+// state is a fixpoint and cand0/cand1 hold every empty cell's candidates.
+__device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gmask, uint32_t bad,
+                                     uint32_t depth, uint32_t &cand0, uint32_t &cand1, bool &placed)
+{
+    placed = false;
+    // ---- phase A: unit masks of all filled cells; clash detection
+    if (lane < 27) W.M[lane] = gmask;
+    wave_lds_sync();
+    uint32_t clash = 0;
+    if (s.v0 != 0 && !s.g0) {
+        uint32_t bit = 1u << (s.v0 - 1);
+        clash |= (atomicOr(&W.M[s.r0], bit) | atomicOr(&W.M[9 + s.c0], bit) |
+                  atomicOr(&W.M[18 + s.b0], bit)) & bit;
+    }
+    if (s.has1 && s.v1 != 0 && !s.g1) {
+        uint32_t bit = 1u << (s.v1 - 1);
+        clash |= (atomicOr(&W.M[s.r1], bit) | atomicOr(&W.M[9 + s.c1], bit) |
+                  atomicOr(&W.M[18 + s.b1], bit)) & bit;
+    }
+    wave_lds_sync();
+    const bool e0 = s.v0 == 0;
+    const bool e1 = s.has1 && s.v1 == 0;
+    cand0 = e0 ? (~(W.M[s.r0] | W.M[9 + s.c0] | W.M[18 + s.b0]) & 0x1FFu) : 0u;
+    cand1 = e1 ? (~(W.M[s.r1] | W.M[9 + s.c1] | W.M[18 + s.b1]) & 0x1FFu) : 0u;
+    const bool dead = clash != 0 || (e0 && cand0 == 0) || (e1 && cand1 == 0);
+    if (__any(dead)) return PROP_DEAD;
+    if (!__any(e0 || e1)) return PROP_SOLVED;
+
+    // ---- naked singles
+    const bool n0 = e0 && (cand0 & (cand0 - 1)) == 0;
+    const bool n1 = e1 && (cand1 & (cand1 - 1)) == 0;
+    if (__any(n0 || n1)) {
+        if (n0) { s.v0 = __builtin_ctz(cand0) + 1; s.lv0 = depth; }
+        if (n1) { s.v1 = __builtin_ctz(cand1) + 1; s.lv1 = depth; }
+        placed = true;
+        return PROP_OPEN;
+    }
+
+    // ---- phase B: hidden singles and digits with no place in a unit
+    if (lane < 28) { W.O[lane] = 0; W.T[lane] = 0; }
+    wave_lds_sync();
+    if (e0) {
+        uint32_t o;
+        o = atomicOr(&W.O[s.r0], cand0);      atomicOr(&W.T[s.r0], o & cand0);
+        o = atomicOr(&W.O[9 + s.c0], cand0);  atomicOr(&W.T[9 + s.c0], o & cand0);
+        o = atomicOr(&W.O[18 + s.b0], cand0); atomicOr(&W.T[18 + s.b0], o & cand0);
+    }
+    if (e1) {
+        uint32_t o;
+        o = atomicOr(&W.O[s.r1], cand1);      atomicOr(&W.T[s.r1], o & cand1);
+        o = atomicOr(&W.O[9 + s.c1], cand1);  atomicOr(&W.T[9 + s.c1], o & cand1);
+        o = atomicOr(&W.O[18 + s.b1], cand1); atomicOr(&W.T[18 + s.b1], o & cand1);
+    }
+    wave_lds_sync();
+    bool udead = false;
+    if (lane < 27 && !((bad >> lane) & 1u))
+        udead = (W.O[lane] | W.M[lane]) != 0x1FFu;
+    uint32_t h0 = 0, h1 = 0;
+    if (e0) {
+        if (!((bad >> s.r0) & 1u)) h0 |= cand0 & ~W.T[s.r0];
+        if (!((bad >> (9 + s.c0)) & 1u)) h0 |= cand0 & ~W.T[9 + s.c0];
+        if (!((bad >> (18 + s.b0)) & 1u)) h0 |= cand0 & ~W.T[18 + s.b0];
+    }
+    if (e1) {
+        if (!((bad >> s.r1) & 1u)) h1 |= cand1 & ~W.T[s.r1];
+        if (!((bad >> (9 + s.c1)) & 1u)) h1 |= cand1 & ~W.T[9 + s.c1];
+        if (!((bad >> (18 + s.b1)) & 1u)) h1 |= cand1 & ~W.T[18 + s.b1];
+    }
+    const bool dead2 = udead || (h0 & (h0 - 1)) != 0 || (h1 & (h1 - 1)) != 0;
+    if (__any(dead2)) return PROP_DEAD;
+    if (__any(h0 != 0 || h1 != 0)) {
+        if (h0) { s.v0 = __builtin_ctz(h0) + 1; s.lv0 = depth; }
+        if (h1) { s.v1 = __builtin_ctz(h1) + 1; s.lv1 = depth; }
+        placed = true;
+    }
+    return PROP_OPEN;
+}
+
+__device__ __forceinline__ int propagate(WaveLds &W, int lane, Cells &s, uint32_t gmask, uint32_t bad,
+                                         uint32_t depth, uint32_t &cand0, uint32_t &cand1, uint32_t &sweeps)
+{
+    for (;;) {
+        bool placed;
+        int st = sweep(W, lane, s, gmask, bad, depth, cand0, cand1, placed);
+        sweeps++;
+        if (st != PROP_OPEN || !placed) return st;
+    }
+}
+
+// first empty cell (row-major) and its candidates; requires a fixpoint state
+__device__ __forceinline__ void first_empty(const Cells &s, uint32_t cand0, uint32_t cand1, int &cell, uint32_t &cand)
+{
+    const uint64_t eb0 = __ballot(s.v0 == 0);
+    if (eb0) {
+        cell = __builtin_ctzll(eb0);
+        cand = rdlane(cand0, cell);
+    } else {
+        const uint64_t eb1 = __ballot(s.has1 && s.v1 == 0);
+        const int l = __builtin_ctzll(eb1);
+        cell = 64 + l;
+        cand = rdlane(cand1, l);
+    }
+}
+
+__device__ __forceinline__ void place(Cells &s, int lane, int cell, uint32_t dbit, uint32_t level)
+{
+    const uint32_t v = __builtin_ctz(dbit) + 1;
+    if (cell < 64) {
+        if (lane == cell) { s.v0 = v; s.lv0 = level; }
+    } else {
+        if (lane == cell - 64) { s.v1 = v; s.lv1 = level; }
+    }
+}
+
+__device__ __forceinline__ void store_board(uint8_t *__restrict__ dst, int lane, const Cells &s, bool original)
+{
+    uint32_t a = original ? (s.g0 ? s.v0 : 0u) : s.v0;
+    uint32_t b = original ? (s.g1 ? s.v1 : 0u) : s.v1;
+    dst[lane] = (uint8_t)a;
+    if (s.has1) dst[64 + lane] = (uint8_t)b;
+}
+
+// Full search of one board.  Returns SDK_SOLVED / SDK_UNSOLVABLE /
+// SDK_CANCELLED; on SOLVED the cells hold the walk's first solution.
+__device__ __forceinline__ int search(WaveLds &W, int lane, Cells &s, int64_t idx,
+                                      const int64_t *best, uint32_t &guesses, uint32_t &sweeps)
+{
+    uint32_t bad;
+    const uint32_t gmask = build_given_masks(W, lane, s, bad);
+    uint32_t depth = 0;
+    uint32_t stk0 = 0, stk1 = 0;  // DFS stack: level k lives in lane k&63 of stk(k>>6)
+    uint32_t cand0, cand1;
+    for (;;) {
+        int st = propagate(W, lane, s, gmask, bad, depth, cand0, cand1, sweeps);
+        if (st == PROP_SOLVED) return SDK_SOLVED;
+        if (st == PROP_OPEN) {
+            // branch on the first empty cell, smallest digit first
+            int cell;
+            uint32_t cand;
+            first_empty(s, cand0, cand1, cell, cand);
+            const uint32_t d = lowbit(cand);
+            const uint32_t entry = ((uint32_t)cell << 9) | (cand ^ d);
+            if (depth < 64) { if (lane == (int)depth) stk0 = entry; }
+            else if (lane == (int)depth - 64) stk1 = entry;
+            depth++;
+            place(s, lane, cell, d, depth);
+            guesses++;
+            if (best && (guesses & 63u) == 0) {
+                const int64_t b = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if (__builtin_amdgcn_readfirstlane((int)(b < idx))) return SDK_CANCELLED;
+            }
+            continue;
+        }
+        // dead: backtrack to the deepest level with an untried digit
+        for (;;) {
+            if (depth == 0) return SDK_UNSOLVABLE;
+            const uint32_t top = depth - 1;
+            const uint32_t entry = top < 64 ? rdlane(stk0, top) : rdlane(stk1, top - 64);
+            if (s.lv0 >= depth) s.v0 = 0;  // undo everything filled at this depth
+            if (s.lv1 >= depth) s.v1 = 0;
+            depth = top;
+            const uint32_t rem = entry & 0x1FFu;
+            if (rem == 0) continue;
+            const int cell = (int)(entry >> 9);
+            const uint32_t d = lowbit(rem);
+            const uint32_t ne = ((uint32_t)cell << 9) | (rem ^ d);
+            if (depth < 64) { if (lane == (int)depth) stk0 = ne; }
+            else if (lane == (int)depth - 64) stk1 = ne;
+            depth++;
+            place(s, lane, cell, d, depth);
+            guesses++;
+            break;
+        }
+    }
+}
+
+// ------------------------------------------------------------- solve kernel
+// re-arm the per-call workspace words on the stream (graph-capturable)
+__global__ void arm_kernel(unsigned long long *ws)
+{
+    if (threadIdx.x == WS_QUEUE) ws[WS_QUEUE] = 0ull;
+    if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered)
+{
+    __shared__ WaveLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    WaveLds &W = lds[threadIdx.x >> 6];
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+
+    uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
+    // first chunk statically, the rest from the queue
+    int64_t base = gw * chunk;
+    const int64_t static_end = nwaves * chunk;
+    while (base < n) {
+        const int64_t end = base + chunk < n ? base + chunk : n;
+        for (int64_t p = base; p < end; ++p) {
+            Cells s;
+            cell_units(lane, s.r0, s.c0, s.b0);
+            cell_units(lane < 17 ? 64 + lane : 80, s.r1, s.c1, s.b1);
+            const uint8_t *src = puzzles + p * 81;
+            uint8_t *dst = sols + p * 81;
+            int st;
+            if (!load_board(src, lane, s)) {
+                st = SDK_INVALID;
+                store_board(dst, lane, s, false);  // raw input back
+            } else if (best && __builtin_amdgcn_readfirstlane((int)(
+                           __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p))) {
+                st = SDK_CANCELLED;
+                store_board(dst, lane, s, true);
+            } else {
+                st = search(W, lane, s, p, best, guesses, sweeps);
+                store_board(dst, lane, s, st != SDK_SOLVED);
+                if (st == SDK_SOLVED) {
+                    solved++;
+                    if (best && lane == 0)
+                        __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED,
+                                               __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            if (lane == 0) status[p] = st;
+            fin++;
+        }
+        unsigned long long t = 0;
+        if (lane == 0) t = atomicAdd(&ws[WS_QUEUE], 1ull);
+        t = __shfl(t, 0);
+        base = static_end + (int64_t)t * chunk;
+    }
+    if (lane == 0 && fin) {
+        atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
+        atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
+        atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
+        atomicAdd(&ws[WS_SWEEPS], (unsigned long long)sweeps);
+    }
+}
+
+// ------------------------------------------------------------ check kernel
+// One thread per grid; the block stages its 64 grids (5184 B) through LDS
+// with coalesced dword loads.
+#define CHECK_GRIDS 64
+__global__ __launch_bounds__(64) void check_kernel(const uint8_t *__restrict__ grids, int32_t *__restrict__ ok,
+                                                   int64_t n, int mode)
+{
+    __shared__ __attribute__((aligned(16))) uint8_t tile[CHECK_GRIDS * 81 + 16];
+    const int64_t g0 = (int64_t)blockIdx.x * CHECK_GRIDS;
+    const int64_t cnt = n - g0 < CHECK_GRIDS ? n - g0 : CHECK_GRIDS;
+    const uint8_t *src = grids + g0 * 81;
+    const int64_t bytes = cnt * 81;
+    for (int64_t i = threadIdx.x; i < bytes; i += 64) tile[i] = src[i];
+    __syncthreads();
+    if (threadIdx.x >= cnt) return;
+    const uint8_t *g = tile + threadIdx.x * 81;
+    bool good = true;
+    // units: rows, columns, boxes (sudoku.py:125-138 order; result is order-free)
+    for (int u = 0; u < 27 && good; ++u) {
+        int idx[9];
+        if (u < 9) {
+            for (int k = 0; k < 9; ++k) idx[k] = u * 9 + k;
+        } else if (u < 18) {
+            for (int k = 0; k < 9; ++k) idx[k] = k * 9 + (u - 9);
+        } else {
+            const int br = ((u - 18) / 3) * 3, bc = ((u - 18) % 3) * 3;
+            for (int k = 0; k < 9; ++k) idx[k] = (br + k / 3) * 9 + bc + k % 3;
+        }
+        uint32_t sum = 0;
+        for (int k = 0; k < 9; ++k) sum += g[idx[k]];
+        if (sum != 45) { good = false; break; }
+        if (mode == 0) {
+            // len(set(unit)) == 9: all nine bytes pairwise distinct
+            bool distinct = true;
+            for (int a = 0; a < 9; ++a)
+                for (int b = a + 1; b < 9; ++b) distinct &= g[idx[a]] != g[idx[b]];
+            good = distinct;
+        }
+    }
+    ok[g0 + threadIdx.x] = good ? 1 : 0;
+}
+
+// ----------------------------------------------------- first-candidate kernel
+// node.py:76-80 with node.py:42-60's is_valid_move (check() short-circuit).
+__global__ __launch_bounds__(256) void first_candidate_kernel(const uint8_t *__restrict__ grids,
+                                                              const int32_t *__restrict__ cells,
+                                                              int32_t *__restrict__ num, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *g = grids + i * 81;
+    const int cell = cells[i];
+    if (cell < 0 || cell >= 81) { num[i] = -1; return; }
+    // node.py:82-116 sums check
+    bool sums = true;
+    for (int u = 0; u < 27 && sums; ++u) {
+        uint32_t sum = 0;
+        for (int k = 0; k < 9; ++k) {
+            int idx = u < 9 ? u * 9 + k
+                    : u < 18 ? k * 9 + (u - 9)
+                             : (((u - 18) / 3) * 3 + k / 3) * 9 + ((u - 18) % 3) * 3 + k % 3;
+            sum += g[idx];
+        }
+        sums = sum == 45;
+    }
+    if (sums) { num[i] = 1; return; }
+    const int r = cell / 9, c = cell % 9, br = (r / 3) * 3, bc = (c / 3) * 3;
+    uint32_t used = 0;
+    for (int k = 0; k < 9; ++k) {
+        uint32_t a = g[r * 9 + k], b = g[k * 9 + c], x = g[(br + k / 3) * 9 + bc + k % 3];
+        if (a >= 1 && a <= 9) used |= 1u << (a - 1);
+        if (b >= 1 && b <= 9) used |= 1u << (b - 1);
+        if (x >= 1 && x <= 9) used |= 1u << (x - 1);
+    }
+    const uint32_t free_ = ~used & 0x1FFu;
+    num[i] = free_ ? (int32_t)__builtin_ctz(free_) + 1 : 0;
+}
+
+// ------------------------------------------------------ frontier expansion
+// pass 1: propagate each node (one wave each), keep the propagated grid and
+// the number of children it will produce.
+__global__ __launch_bounds__(BLOCK_THREADS) void expand_count_kernel(const uint8_t *__restrict__ nodes, int64_t n,
+                                                                     uint8_t *__restrict__ tmp,
+                                                                     int64_t *__restrict__ counts)
+{
+    __shared__ WaveLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    WaveLds &W = lds[threadIdx.x >> 6];
+    const int64_t p = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (p >= n) return;
+    Cells s;
+    cell_units(lane, s.r0, s.c0, s.b0);
+    cell_units(lane < 17 ? 64 + lane : 80, s.r1, s.c1, s.b1);
+    uint8_t *dst = tmp + p * 81;
+    int64_t cnt = 0;
+    if (load_board(nodes + p * 81, lane, s)) {
+        uint32_t bad;
+        const uint32_t gmask = build_given_masks(W, lane, s, bad);
+        uint32_t cand0, cand1, sweeps = 0;
+        const int st = propagate(W, lane, s, gmask, bad, 0, cand0, cand1, sweeps);
+        if (st == PROP_SOLVED) {
+            cnt = 1;
+        } else if (st == PROP_OPEN) {
+            int cell;
+            uint32_t cand;
+            first_empty(s, cand0, cand1, cell, cand);
+            cnt = __builtin_popcount(cand);
+        }
+    }
+    store_board(dst, lane, s, false);
+    if (lane == 0) counts[p] = cnt;
+}
+
+// exclusive scan of counts -> offsets (n+1 entries), one block
+__global__ __launch_bounds__(1024) void scan_kernel(const int64_t *__restrict__ counts, int64_t *__restrict__ offsets,
+                                                    int64_t n)
+{
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (n + 1023) / 1024;
+    const int64_t lo = t * per, hi = lo + per < n ? lo + per : n;
+    int64_t s = 0;
+    for (int64_t i = lo; i < hi; ++i) s += counts[i];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        int64_t run = 0;
+        for (int k = 0; k < 1024; ++k) { int64_t v = part[k]; part[k] = run; run += v; }
+        offsets[n] = run;
+    }
+    __syncthreads();
+    int64_t run = part[t];
+    for (int64_t i = lo; i < hi; ++i) {  // in place: read the count before overwriting it
+        const int64_t c = counts[i];
+        offsets[i] = run;
+        run += c;
+    }
+}
+
+// pass 2: write children (one wave per node) in digit order
+__global__ __launch_bounds__(BLOCK_THREADS) void expand_write_kernel(const uint8_t *__restrict__ tmp, int64_t n,
+                                                                     const int64_t *__restrict__ offsets,
+                                                                     uint8_t *__restrict__ children, int64_t cap)
+{
+    const int lane = threadIdx.x & 63;
+    const int64_t p = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    if (p >= n) return;
+    const int64_t off = offsets[p], cnt = offsets[p + 1] - off;
+    if (cnt == 0) return;
+    const uint8_t *g = tmp + p * 81;
+    const uint32_t a = g[lane];
+    const uint32_t b = lane < 17 ? g[64 + lane] : 1u;
+    // candidates of the first empty cell recomputed from the grid itself
+    const uint64_t eb0 = __ballot(a == 0);
+    const uint64_t eb1 = __ballot(lane < 17 && b == 0);
+    int cell = eb0 ? __builtin_ctzll(eb0) : (eb1 ? 64 + __builtin_ctzll(eb1) : -1);
+    uint32_t used = 0;
+    if (cell >= 0) {
+        const int r = cell / 9, c = cell % 9, br = (r / 3) * 3, bc = (c / 3) * 3;
+        // lanes 0..8 read row / column / box members, OR-reduce
+        uint32_t m = 0;
+        if (lane < 9) {
+            uint32_t x = g[r * 9 + lane], y = g[lane * 9 + c], z = g[(br + lane / 3) * 9 + bc + lane % 3];
+            if (x) m |= 1u << (x - 1);
+            if (y) m |= 1u << (y - 1);
+            if (z) m |= 1u << (z - 1);
+        }
+        for (int sh = 1; sh < 16; sh <<= 1) m |= __shfl_xor(m, sh);
+        used = rdlane(m, 0);
+    }
+    uint32_t cand = cell >= 0 ? (~used & 0x1FFu) : 0u;
+    for (int64_t k = 0; k < cnt; ++k) {
+        const int64_t o = off + k;
+        if (o >= cap) break;
+        uint8_t *dst = children + o * 81;
+        uint32_t va = a, vb = b;
+        if (cell >= 0) {
+            const uint32_t d = __builtin_ctz(cand) + 1;
+            cand &= cand - 1;
+            if (cell < 64) { if (lane == cell) va = d; }
+            else if (lane == cell - 64) vb = d;
+        }
+        dst[lane] = (uint8_t)va;
+        if (lane < 17) dst[64 + lane] = (uint8_t)vb;
+    }
+}
+
+// ==================================================================== C ABI
+static thread_local char g_err[512];
+static std::mutex g_mu;
+static int g_cu_count[64];
+
+static int set_err(const char *what, hipError_t e)
+{
+    snprintf(g_err, sizeof g_err, "%s: %s", what, hipGetErrorString(e));
+    return -1;
+}
+
+static int cu_count()
+{
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (!g_cu_count[dev]) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+        g_cu_count[dev] = v;
+    }
+    return g_cu_count[dev];
+}
+
+extern "C" {
+
+const char *sdk_last_error(void) { return g_err; }
+const char *sdk_version(void) { return "sudoku_hip 0.1 gfx950 wave-per-board lex-order"; }
+int sdk_device_cu_count(void) { return cu_count(); }
+size_t sdk_workspace_bytes(void) { return WS_WORDS * sizeof(unsigned long long); }
+
+int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
+                    void *d_workspace, int ordered, void *stream)
+{
+    if (n < 0 || (n > 0 && (!d_puzzles || !d_solutions || !d_status || !d_workspace))) {
+        snprintf(g_err, sizeof g_err, "sdk_solve_batch: bad arguments (n=%lld)", (long long)n);
+        return -2;
+    }
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long *ws = (unsigned long long *)d_workspace;
+    hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
+    hipError_t e;
+    // persistent grid: up to 8 waves per SIMD (32 per CU)
+    const int64_t max_waves = (int64_t)cu_count() * 32;
+    int64_t waves = n < max_waves ? n : max_waves;
+    int64_t chunk = n / (waves * 16);
+    if (chunk < 1) chunk = 1;
+    if (chunk > 16) chunk = 16;
+    const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+    hipLaunchKernelGGL(solve_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
+                       d_status, n, ws, chunk, ordered);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err("sdk_solve_batch: launch", e);
+    return 0;
+}
+
+int sdk_check_batch(const uint8_t *d_grids, int32_t *d_ok, int64_t n, int mode, void *stream)
+{
+    if (n < 0 || (n > 0 && (!d_grids || !d_ok)) || (mode != 0 && mode != 1)) {
+        snprintf(g_err, sizeof g_err, "sdk_check_batch: bad arguments");
+        return -2;
+    }
+    if (n == 0) return 0;
+    const int64_t blocks = (n + CHECK_GRIDS - 1) / CHECK_GRIDS;
+    hipLaunchKernelGGL(check_kernel, dim3((unsigned)blocks), dim3(64), 0, (hipStream_t)stream, d_grids, d_ok, n, mode);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_check_batch: launch", e);
+}
+
+int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells, int32_t *d_num, int64_t n,
+                              void *stream)
+{
+    if (n < 0 || (n > 0 && (!d_grids || !d_cells || !d_num))) {
+        snprintf(g_err, sizeof g_err, "sdk_first_candidate_batch: bad arguments");
+        return -2;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(first_candidate_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                       d_grids, d_cells, d_num, n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_first_candidate_batch: launch", e);
+}
+
+int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64_t *d_offsets,
+                        uint8_t *d_children, int64_t cap, void *stream)
+{
+    if (n < 0 || cap < 0 || (n > 0 && (!d_nodes || !d_tmp || !d_offsets || (cap > 0 && !d_children)))) {
+        snprintf(g_err, sizeof g_err, "sdk_expand_frontier: bad arguments");
+        return -2;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    if (n == 0) {
+        hipError_t e = hipMemsetAsync(d_offsets, 0, sizeof(int64_t), st);
+        return e == hipSuccess ? 0 : set_err("sdk_expand_frontier: memset", e);
+    }
+    const unsigned blocks = (unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
+    // per-node child counts are written into d_offsets[0..n) and scanned in place
+    hipLaunchKernelGGL(expand_count_kernel, dim3(blocks), dim3(BLOCK_THREADS), 0, st, d_nodes, n, d_tmp, d_offsets);
+    hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, d_offsets, d_offsets, n);
+    hipLaunchKernelGGL(expand_write_kernel, dim3(blocks), dim3(BLOCK_THREADS), 0, st, d_tmp, n, d_offsets,
+                       d_children, cap);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_expand_frontier: launch", e);
+}
+
+int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
+{
+    if (!d_workspace || !out) {
+        snprintf(g_err, sizeof g_err, "sdk_read_stats: bad arguments");
+        return -2;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long h[WS_WORDS];
+    hipError_t e = hipMemcpyAsync(h, d_workspace, sizeof h, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_err("sdk_read_stats", e);
+    out[0] = (int64_t)h[WS_FINISHED];
+    out[1] = (int64_t)h[WS_SOLVED];
+    out[2] = (int64_t)h[WS_GUESSES];
+    out[3] = (int64_t)h[WS_SWEEPS];
+    out[4] = (int64_t)h[WS_BEST];
+    out[5] = 0;
+    if (reset) {
+        e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 4 * sizeof(unsigned long long), st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e != hipSuccess) return set_err("sdk_read_stats: reset", e);
+    }
+    return 0;
+}
+
+}  // extern "C"

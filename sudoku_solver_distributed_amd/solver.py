@@ -1,0 +1,194 @@
+"""Device-side batch API over the C ABI (include/sudoku_hip.h).
+
+PyTorch is plumbing here: it owns device memory, streams and
+``torch.distributed``; all Sudoku work runs in libsudoku_hip.so.  Nothing in
+this module falls back to a CPU path -- without a GPU or without the library
+every call raises.
+
+Boards are ``uint8`` tensors of shape ``(n, 81)`` (row-major, 0 = empty).
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import SDK_CANCELLED, SDK_INVALID, SDK_SOLVED, SDK_UNSOLVABLE, SudokuHipError
+
+__all__ = [
+    "BatchSolver", "get_solver", "as_boards", "SDK_SOLVED", "SDK_UNSOLVABLE",
+    "SDK_INVALID", "SDK_CANCELLED", "SudokuHipError",
+]
+
+
+def _require_gpu(device) -> torch.device:
+    if not torch.cuda.is_available():
+        raise SudokuHipError("no ROCm GPU visible: the Sudoku solver runs only on the HIP path")
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if dev.type != "cuda":
+        raise SudokuHipError(f"device {dev} is not a GPU device")
+    if dev.index is None:
+        dev = torch.device("cuda", torch.cuda.current_device())
+    return dev
+
+
+def as_boards(x, device=None) -> torch.Tensor:
+    """Anything board-like -> contiguous (n, 81) uint8 tensor (host or device).
+
+    Accepts a 9x9 list of lists (the reference's board type), a list of such
+    boards, an 81-char string, numpy arrays and tensors.  Raises ValueError on
+    a cell outside 0..9 (the reference would silently compare such values;
+    this boundary rejects them up front)."""
+    if isinstance(x, str):
+        x = [int(c) for c in x]
+    if isinstance(x, torch.Tensor):
+        t = x
+    else:
+        a = np.asarray(x)
+        if a.dtype == object:
+            raise ValueError("ragged board")
+        if a.size and (a.min() < 0 or a.max() > 9):
+            raise ValueError("board cells must be integers 0..9")
+        t = torch.from_numpy(np.ascontiguousarray(a.astype(np.uint8)))
+    if t.numel() % 81 != 0:
+        raise ValueError(f"board data of {t.numel()} cells is not a multiple of 81")
+    t = t.reshape(-1, 81)
+    if t.dtype != torch.uint8:
+        if t.numel() and (int(t.min()) < 0 or int(t.max()) > 9):
+            raise ValueError("board cells must be integers 0..9")
+        t = t.to(torch.uint8)
+    if device is not None:
+        t = t.to(device, non_blocking=True)
+    return t.contiguous()
+
+
+class BatchSolver:
+    """One per device.  Holds the small device workspace of the C ABI."""
+
+    def __init__(self, device=None):
+        self.device = _require_gpu(device)
+        self.lib = _lib.load()
+        with torch.cuda.device(self.device):
+            self.workspace = torch.zeros(int(self.lib.sdk_workspace_bytes()), dtype=torch.uint8,
+                                         device=self.device)
+
+    # ------------------------------------------------------------ helpers
+    def _stream(self, stream) -> int:
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return int(s.cuda_stream)
+
+    def _dev(self, t: torch.Tensor) -> torch.Tensor:
+        if t.device != self.device:
+            t = t.to(self.device)
+        return t.contiguous()
+
+    # -------------------------------------------------------------- solve
+    def solve(self, puzzles, out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
+              ordered: bool = False, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Solve every board (gen.py:6-28 semantics).  Asynchronous on the
+        stream; returns (solutions uint8 (n,81), status int32 (n,))."""
+        p = self._dev(as_boards(puzzles))
+        n = p.shape[0]
+        if out is None:
+            out = torch.empty_like(p)
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32, device=self.device)
+        if out.shape != p.shape or out.dtype != torch.uint8 or not out.is_contiguous():
+            raise ValueError("out must be a contiguous (n, 81) uint8 tensor")
+        if status.shape != (n,) or status.dtype != torch.int32:
+            raise ValueError("status must be an (n,) int32 tensor")
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_solve_batch(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
+                                          self.workspace.data_ptr(), 1 if ordered else 0,
+                                          self._stream(stream))
+        _lib.check(rc, "sdk_solve_batch")
+        return out, status
+
+    def check(self, grids, mode: int = 0, stream=None) -> torch.Tensor:
+        """mode 0: Sudoku.check (sudoku.py:119-140); mode 1: node.py:82-116."""
+        g = self._dev(as_boards(grids))
+        ok = torch.empty(g.shape[0], dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_check_batch(g.data_ptr(), ok.data_ptr(), g.shape[0], mode, self._stream(stream))
+        _lib.check(rc, "sdk_check_batch")
+        return ok
+
+    def first_candidate(self, grids, cells, stream=None) -> torch.Tensor:
+        """node.py:76-80 per (board, cell) task; 0 means None."""
+        g = self._dev(as_boards(grids))
+        c = self._dev(torch.as_tensor(cells, dtype=torch.int32).reshape(-1))
+        if c.shape[0] != g.shape[0]:
+            raise ValueError("one cell index per board")
+        num = torch.empty(g.shape[0], dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_first_candidate_batch(g.data_ptr(), c.data_ptr(), num.data_ptr(), g.shape[0],
+                                                    self._stream(stream))
+        _lib.check(rc, "sdk_first_candidate_batch")
+        return num
+
+    def expand(self, nodes, stream=None) -> torch.Tensor:
+        """One frontier level (sdk_expand_frontier); synchronises to size it."""
+        nd = self._dev(as_boards(nodes))
+        n = nd.shape[0]
+        tmp = torch.empty_like(nd)
+        offsets = torch.empty(n + 1, dtype=torch.int64, device=self.device)
+        cap = 9 * n
+        children = torch.empty((max(cap, 1), 81), dtype=torch.uint8, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_expand_frontier(nd.data_ptr(), n, tmp.data_ptr(), offsets.data_ptr(),
+                                              children.data_ptr(), cap, self._stream(stream))
+        _lib.check(rc, "sdk_expand_frontier")
+        total = int(offsets[n].item()) if n else 0
+        if total > cap:
+            raise SudokuHipError(f"frontier overflow: {total} > {cap}")
+        return children[:total]
+
+    def stats(self, reset: bool = False, stream=None) -> dict:
+        out = (ctypes.c_int64 * 6)()
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_read_stats(self.workspace.data_ptr(), out, 1 if reset else 0, self._stream(stream))
+        _lib.check(rc, "sdk_read_stats")
+        return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4]}
+
+    # ------------------------------------------------------ frontier split
+    def frontier(self, board, target: int = 4096, max_levels: int = 81) -> torch.Tensor:
+        """Expand one board's search tree (in the walk's order) until the
+        frontier holds >= target nodes or cannot grow."""
+        nodes = self._dev(as_boards(board))
+        for _ in range(max_levels):
+            if nodes.shape[0] >= target or nodes.shape[0] == 0:
+                break
+            children = self.expand(nodes)
+            if children.shape[0] == nodes.shape[0] and torch.equal(children, nodes):
+                break  # every node already solved: nothing left to split
+            nodes = children
+        return nodes
+
+    def solve_one_split(self, board, target: int = 4096) -> Tuple[bool, torch.Tensor]:
+        """Single hard board: frontier split over all waves of this GPU, then
+        an ordered solve; returns (solved, grid81)."""
+        root = self._dev(as_boards(board))
+        if root.shape[0] != 1:
+            raise ValueError("solve_one_split takes exactly one board")
+        nodes = self.frontier(root, target)
+        if nodes.shape[0] == 0:
+            return False, root[0].clone()
+        sols, st = self.solve(nodes, ordered=True)
+        hit = torch.nonzero(st == SDK_SOLVED)
+        if hit.numel() == 0:
+            return False, root[0].clone()
+        return True, sols[int(hit[0, 0].item())].clone()
+
+
+_SOLVERS = {}
+
+
+def get_solver(device=None) -> BatchSolver:
+    dev = _require_gpu(device)
+    s = _SOLVERS.get(dev.index)
+    if s is None:
+        s = _SOLVERS[dev.index] = BatchSolver(dev)
+    return s

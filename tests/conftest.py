@@ -1,0 +1,35 @@
+import json
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path)")
+    config.addinivalue_line("markers", "slow: long-running CPU case")
+
+
+def load_golden(name):
+    with open(os.path.join(GOLDEN, name)) as f:
+        return json.load(f)
+
+
+def b81(s):
+    return [int(c) for c in s]
+
+
+def grid9(s):
+    return [[int(s[r * 9 + c]) for c in range(9)] for r in range(9)]
+
+
+@pytest.fixture(scope="session")
+def solver():
+    from sudoku_solver_distributed_amd.solver import get_solver
+    return get_solver()

@@ -1,0 +1,58 @@
+"""C ABI: the library loads without a GPU and exports every symbol that
+include/sudoku_hip.h declares (no compute calls here)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    with open(os.path.join(ROOT, "include", "sudoku_hip.h")) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(sdk_[a-z_0-9]+)\s*\(", text)))
+
+
+def test_header_declares_entry_points():
+    names = _declared()
+    assert "sdk_solve_batch" in names and "sdk_check_batch" in names
+    from sudoku_solver_distributed_amd import _lib
+    assert sorted(_lib.EXPORTS) == names
+
+
+def test_library_exports_all_symbols():
+    from sudoku_solver_distributed_amd import _lib, build
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    for name in _declared():
+        assert hasattr(lib, name), name
+    L = _lib.load()
+    assert L.sdk_workspace_bytes() >= 64
+    assert b"gfx950" in L.sdk_version()
+
+
+def test_code_object_is_gfx950():
+    from sudoku_solver_distributed_amd import _lib
+    with open(_lib.LIB_PATH, "rb") as f:
+        blob = f.read()
+    assert b"gfx950" in blob
+
+
+def test_product_does_not_import_oracle():
+    pkg = os.path.join(ROOT, "sudoku_solver_distributed_amd")
+    for dirpath, _, files in os.walk(pkg):
+        for fn in files:
+            if fn.endswith(".py"):
+                with open(os.path.join(dirpath, fn)) as f:
+                    src = f.read()
+                assert "oracle" not in re.sub(r"#.*", "", src).replace("oracle/", ""), fn
+
+
+def test_solver_raises_without_gpu():
+    import pytest
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    from sudoku_solver_distributed_amd.solver import BatchSolver, SudokuHipError
+    with pytest.raises(SudokuHipError):
+        BatchSolver()

@@ -1,0 +1,208 @@
+"""HIP path vs oracle / reference golden vectors (runs on an MI355X).
+
+Bar: bit-exact boards and statuses.  Full-size cases (BASELINE.json's 1M
+hard batch) are checked through size-independent properties: every status
+SOLVED, every output passes Sudoku.check, every given preserved, and a
+sampled subset equal to the oracle's unique completion.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import b81, load_golden
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _s(row):
+    return "".join(str(int(v)) for v in row)
+
+
+def test_library_is_native(solver):
+    from sudoku_solver_distributed_amd import _lib
+    assert solver.lib is _lib.load()
+    assert b"gfx950" in solver.lib.sdk_version()
+    assert solver.lib.sdk_device_cu_count() > 0
+
+
+def test_golden_gen(solver):
+    cases = load_golden("golden_gen.json")
+    p = torch.tensor([b81(c["puzzle"]) for c in cases], dtype=torch.uint8)
+    sols, st = solver.solve(p)
+    sols, st = sols.cpu().numpy(), st.cpu().numpy()
+    for c, o, s in zip(cases, sols, st):
+        assert (s == 1) == c["solved"], c["seed"]
+        assert _s(o) == c["solution"], (c["seed"], c["empty_boxes"])
+
+
+def test_golden_named(solver):
+    for c in load_golden("golden_solve.json"):
+        sols, st = solver.solve(torch.tensor([b81(c["puzzle"])], dtype=torch.uint8))
+        assert (int(st[0]) == 1) == c["solved"], c["name"]
+        assert _s(sols[0].cpu()) == c["solution"], c["name"]
+
+
+def test_random_generated_vs_oracle(solver):
+    from sudoku_solver_distributed_amd.gen import generate_batch
+    for empties, n in ((30, 256), (50, 256), (58, 256), (64, 128), (70, 64), (81, 4)):
+        puzzles = generate_batch(n, empties, seed=1234 + empties)
+        sols, st = solver.solve(puzzles)
+        want, wst = O.solve_batch(puzzles.cpu().numpy())
+        assert np.array_equal(st.cpu().numpy(), wst), empties
+        assert np.array_equal(sols.cpu().numpy(), want), empties
+
+
+def test_generate_batch_matches_sequential(solver):
+    import random
+    from sudoku_solver_distributed_amd.gen import generate_batch, generate_sudoku
+    batch = generate_batch(6, 45, seed=99).cpu().numpy()
+    random.seed(99)
+    seq = [generate_sudoku(45) for _ in range(6)]
+    for b, s in zip(batch, seq):
+        assert _s(b) == "".join(str(v) for r in s.grid for v in r)
+
+
+def test_generate_matches_reference_golden(solver):
+    import random
+    from sudoku_solver_distributed_amd.gen import generate_sudoku
+    for c in load_golden("golden_gen.json")[:24]:
+        random.seed(c["seed"])
+        s = generate_sudoku(c["empty_boxes"])
+        assert "".join(str(v) for r in s.grid for v in r) == c["puzzle"]
+
+
+def test_hard17_vs_unique_oracle(solver):
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    p = hard17_batch(384, seed=5)
+    sols, st = solver.solve(p)
+    want, cnt = O.solve_unique_batch(p.numpy())
+    assert (cnt == 1).all()
+    assert (st.cpu().numpy() == 1).all()
+    assert np.array_equal(sols.cpu().numpy(), want)
+
+
+def test_seeds_vs_literal_walk(solver):
+    """Every 17-clue seed against the literal walk (oracle_solve, seconds each)."""
+    from sudoku_solver_distributed_amd.gen import SEEDS_17
+    p = np.array([b81(s) for s in SEEDS_17], dtype=np.uint8)
+    sols, st = solver.solve(torch.from_numpy(p))
+    want, wst = O.solve_batch(p)
+    assert np.array_equal(sols.cpu().numpy(), want)
+    assert np.array_equal(st.cpu().numpy(), wst)
+
+
+def test_edge_cases(solver):
+    full = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
+    bad_full = "5" * 81
+    dead = "123456780000000009" + "0" * 63
+    dup = "550000000" + "0" * 72
+    boards = [full, bad_full, dead, dup, "0" * 81]
+    p = np.array([b81(s) for s in boards], dtype=np.uint8)
+    sols, st = solver.solve(torch.from_numpy(p))
+    want, wst = O.solve_batch(p)
+    assert np.array_equal(st.cpu().numpy(), wst)
+    assert np.array_equal(sols.cpu().numpy(), want)
+    # empty batch
+    s0, t0 = solver.solve(torch.empty((0, 81), dtype=torch.uint8))
+    assert s0.shape == (0, 81) and t0.shape == (0,)
+
+
+def test_invalid_bytes_rejected(solver):
+    from sudoku_solver_distributed_amd.solver import as_boards
+    with pytest.raises(ValueError):
+        as_boards([10] + [0] * 80)
+    # raw ABI path: status SDK_INVALID, output = input
+    raw = torch.zeros((2, 81), dtype=torch.uint8, device=solver.device)
+    raw[1, 5] = 12
+    sols, st = solver.solve(raw)
+    assert st.cpu().tolist() == [1, -1]
+    assert int(sols[1, 5]) == 12
+
+
+def test_duplicate_givens_vs_oracle(solver):
+    rng = np.random.default_rng(3)
+    from sudoku_solver_distributed_amd.gen import generate_batch
+    base = generate_batch(200, 55, seed=77).cpu().numpy()
+    # inject one clashing given into each board
+    for b in base:
+        i, j = rng.choice(81, 2, replace=False)
+        if b[i] == 0:
+            b[i] = rng.integers(1, 10)
+        b[j] = b[i]
+    sols, st = solver.solve(torch.from_numpy(base))
+    want, wst = O.solve_batch(base)
+    assert np.array_equal(st.cpu().numpy(), wst)
+    assert np.array_equal(sols.cpu().numpy(), want)
+
+
+def test_check_batch(solver):
+    cases = load_golden("golden_check.json")
+    g = torch.tensor([b81(c["grid"]) for c in cases], dtype=torch.uint8)
+    ok0 = solver.check(g, 0).cpu().tolist()
+    ok1 = solver.check(g, 1).cpu().tolist()
+    assert ok0 == [int(c["check"]) for c in cases]
+    assert ok1 == [int(c["node_check"]) for c in cases]
+
+
+def test_first_candidate(solver):
+    cases = load_golden("golden_node.json")["first_candidate"]
+    g = torch.tensor([b81(c["grid"]) for c in cases], dtype=torch.uint8)
+    cells = [c["row"] * 9 + c["col"] for c in cases]
+    got = solver.first_candidate(g, cells).cpu().tolist()
+    assert got == [c["num"] or 0 for c in cases]
+
+
+def test_frontier_order_and_split(solver):
+    from sudoku_solver_distributed_amd.gen import PATHOLOGICAL
+    root = torch.tensor([b81(PATHOLOGICAL)], dtype=torch.uint8)
+    nodes = solver.frontier(root, target=512)
+    assert nodes.shape[0] >= 64
+    # frontier nodes are in the walk's order: lexicographically increasing
+    a = nodes.cpu().numpy()
+    for i in range(a.shape[0] - 1):
+        d = np.nonzero(a[i] != a[i + 1])[0]
+        assert d.size and 0 < a[i, d[0]] < a[i + 1, d[0]]
+    ok, grid = solver.solve_one_split(root, target=2048)
+    want, cnt = O.solve_unique_batch(np.array([b81(PATHOLOGICAL)], dtype=np.uint8))
+    assert ok and cnt[0] == 1
+    assert np.array_equal(grid.cpu().numpy(), want[0])
+
+
+def test_ordered_mode_picks_lowest(solver):
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    p = hard17_batch(64, seed=11)
+    p[:10, :] = torch.tensor(b81("123456780000000009" + "0" * 63), dtype=torch.uint8)  # dead boards
+    sols, st = solver.solve(p, ordered=True)
+    st = st.cpu().numpy()
+    assert (st[:10] == 0).all()
+    assert st[10] == 1
+    assert set(np.unique(st[11:])) <= {1, -2}
+    assert solver.stats()["best"] == 10
+
+
+def test_full_size_properties(solver):
+    """BASELINE.json configs[2] shape on one GPU: 1M hard 17-clue boards."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    n = 1 << 20
+    p = hard17_batch(n, seed=2024, device=solver.device)
+    sols, st = solver.solve(p)
+    assert bool((st == 1).all())
+    assert bool((solver.check(sols, 0) == 1).all())
+    givens = p != 0
+    assert bool((sols[givens] == p[givens]).all())
+    idx = torch.randint(0, n, (128,), generator=torch.Generator().manual_seed(1))
+    want, cnt = O.solve_unique_batch(p[idx.to(p.device)].cpu().numpy())
+    assert np.array_equal(sols[idx.to(p.device)].cpu().numpy(), want)
+
+
+def test_sudoku_class_api(solver):
+    from sudoku_solver_distributed_amd.sudoku import Sudoku
+    from sudoku_solver_distributed_amd.gen import solve_sudoku
+    c = load_golden("golden_solve.json")[0]
+    board = [[int(c["puzzle"][r * 9 + k]) for k in range(9)] for r in range(9)]
+    assert solve_sudoku(board) == c["solved"]
+    assert "".join(str(v) for r in board for v in r) == c["solution"]
+    assert Sudoku(board).check() is True
+    board[0][0], board[0][1] = board[0][1], board[0][0]
+    assert Sudoku(board).check() is False
