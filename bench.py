@@ -54,6 +54,8 @@ def main():
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--latency-boards", type=int, default=32,
+                    help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
     args = ap.parse_args()
 
     import torch
@@ -110,7 +112,7 @@ def main():
 
     # single-board latency (p50 over 32 boards, one launch each)
     lat = []
-    for i in range(32):
+    for i in range(args.latency_boards):
         b = boards[i:i + 1]
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()
@@ -118,7 +120,7 @@ def main():
         torch.cuda.synchronize(dev)
         lat.append((time.perf_counter() - s0) * 1e3)
     lat.sort()
-    p50 = lat[len(lat) // 2]
+    p50 = lat[len(lat) // 2] if lat else None
 
     if rank != 0:
         if world > 1:

@@ -29,6 +29,12 @@ extern "C" {
 #define SDK_SOLVED 1      /* gen.py:18/25 `return True`; output = filled board */
 #define SDK_INVALID -1    /* a byte > 9 in the input (rejected, output = input) */
 #define SDK_CANCELLED -2  /* ordered mode: a lower-indexed board already solved */
+#define SDK_FAULT -3      /* internal consistency check failed (never expected) */
+
+/* the reference's two walks (cell choice; digits are always tried 1..9) */
+#define SDK_ORDER_GEN 0   /* gen.py:6-28: first empty cell of the LAST row that
+                             has one (its scan breaks only the inner loop) */
+#define SDK_ORDER_NODE 1  /* node.py:62-74: first empty cell, row-major      */
 
 /* Bytes of device workspace sdk_solve_batch needs (queue heads, cancel word,
  * statistics).  Allocate once, zero once; the library re-arms the per-call
@@ -36,16 +42,17 @@ extern "C" {
 size_t sdk_workspace_bytes(void);
 
 /* Solve n boards.  For every board the output is the FIRST solution of the
- * reference's backtracking walk -- first empty cell in row-major order,
- * digits 1..9 ascending -- i.e. bit-identical to
- *   gen.py:6-28        solve_sudoku(board)
- *   node.py:31-40,62-74 SudokuSolver.solve_sudoku / solve_sudoku_recursive
- * (node.py differs only on boards whose givens already clash).
- * d_puzzles and d_solutions may alias.  `ordered` != 0 selects frontier mode:
- * once board i is solved, boards j > i are abandoned (status SDK_CANCELLED)
- * and the lowest solved index is kept in the workspace (sdk_read_stats).  */
+ * reference walk selected by `order`:
+ *   SDK_ORDER_GEN  gen.py:6-28          solve_sudoku(board)
+ *   SDK_ORDER_NODE node.py:31-40,62-74  SudokuSolver.solve_sudoku
+ * bit-identical (node.py additionally short-circuits is_valid_move on boards
+ * whose every unit already sums to 45 -- only boards with clashing givens
+ * can reach that).  d_puzzles and d_solutions may alias.
+ * `ordered` != 0 selects frontier mode: once board i is solved, boards j > i
+ * are abandoned (status SDK_CANCELLED) and the lowest solved index is kept in
+ * the workspace (sdk_read_stats out[4]). */
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status,
-                    int64_t n, void *d_workspace, int ordered, void *stream);
+                    int64_t n, void *d_workspace, int order, int ordered, void *stream);
 
 /* Batch Sudoku.check (mode 0, sudoku.py:119-140: every row, column and box
  * sums to 45 and holds 9 distinct values) or node.py's SudokuSolver.check
@@ -64,7 +71,7 @@ int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
  * re-designed as a frontier split).  Every input node is propagated; then
  *   dead   -> no child,
  *   solved -> one child: the solved grid,
- *   open   -> one child per candidate of its first empty cell (row-major),
+ *   open   -> one child per candidate of the walk's next cell (`order`),
  *             digits ascending.
  * Children of all nodes, concatenated in input order, are therefore in the
  * walk's (lexicographic) order, and the first SOLVED child of the frontier
@@ -74,7 +81,7 @@ int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
  *   d_children: capacity cap*81 bytes; children past cap are not written.
  * Caller checks d_offsets[n] <= cap. */
 int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64_t *d_offsets,
-                        uint8_t *d_children, int64_t cap, void *stream);
+                        uint8_t *d_children, int64_t cap, int order, void *stream);
 
 /* Copy statistics to host (synchronous on `stream`):
  * out[0] boards finished, out[1] boards solved, out[2] guesses (DFS nodes),

@@ -16,8 +16,12 @@
  *   oracle_check           <- sudoku.py:80-140  Sudoku.check_row/column/square/check
  *   oracle_check_sums      <- node.py:82-116    SudokuSolver.check (sums only)
  *   oracle_is_valid_move   <- node.py:42-60     SudokuSolver.is_valid_move
- *   oracle_solve           <- gen.py:6-28       solve_sudoku (row-major, 1..9)
+ *   oracle_solve           <- gen.py:6-28       solve_sudoku; NOTE its cell scan
+ *                             (gen.py:11-15) `break`s only the inner loop, so it
+ *                             branches on the first empty cell of the LAST row
+ *                             holding one: rows 8..0, columns 0..8 ("gen order")
  *   oracle_solve_node      <- node.py:62-74     SudokuSolver.solve_sudoku_recursive
+ *                             (first empty cell row-major: "node order")
  *   oracle_first_candidate <- node.py:76-80     SudokuSolver.solve_sudoku_destributed
  *   oracle_count_solutions    (test helper: uniqueness of generated puzzles)
  */
@@ -109,20 +113,40 @@ typedef int (*valid_fn)(const uint8_t *, int, int, int);
 
 static uint64_t g_nodes; /* candidate tests (the reference's "validations") */
 
-/* gen.py:6-28 -- first empty cell in row-major order, digits 1..9 ascending,
- * recursion; the board is restored to its input on failure. */
-static int solve_rec(uint8_t *g, valid_fn valid)
+/* gen.py:11-15: `for i: for j: if empty: row, col = i, j; break` -- the
+ * break leaves only the column loop, so the LAST row with an empty cell wins,
+ * at its first empty column. */
+static int gen_order_cell(const uint8_t *g)
 {
     int cell = -1;
+    for (int i = 0; i < 9; i++)
+        for (int j = 0; j < 9; j++)
+            if (g[i * 9 + j] == 0) { cell = i * 9 + j; break; }
+    return cell;
+}
+
+/* node.py:63-65: first empty cell in row-major order (the loop returns). */
+static int node_order_cell(const uint8_t *g)
+{
     for (int i = 0; i < 81; i++)
-        if (g[i] == 0) { cell = i; break; }
+        if (g[i] == 0) return i;
+    return -1;
+}
+
+typedef int (*cell_fn)(const uint8_t *);
+
+/* gen.py:6-28 / node.py:62-74 -- pick the branch cell, digits 1..9 ascending,
+ * recursion; the board is restored to its input on failure. */
+static int solve_rec(uint8_t *g, valid_fn valid, cell_fn pick)
+{
+    int cell = pick(g);
     if (cell < 0) return 1;
     int row = cell / 9, col = cell % 9;
     for (int num = 1; num <= 9; num++) {
         g_nodes++;
         if (valid(g, row, col, num)) {
             g[cell] = (uint8_t)num;
-            if (solve_rec(g, valid)) return 1;
+            if (solve_rec(g, valid, pick)) return 1;
             g[cell] = 0;
         }
     }
@@ -131,13 +155,20 @@ static int solve_rec(uint8_t *g, valid_fn valid)
 
 int oracle_solve(uint8_t *g)
 {
-    return solve_rec(g, oracle_is_valid);
+    return solve_rec(g, oracle_is_valid, gen_order_cell);
+}
+
+/* gen.py's test (sudoku.py:60-78) with node.py's cell order: the kernel's
+ * SDK_ORDER_NODE on boards whose givens do not clash. */
+int oracle_solve_rowmajor(uint8_t *g)
+{
+    return solve_rec(g, oracle_is_valid, node_order_cell);
 }
 
 /* node.py:62-74 (same walk, node.py's is_valid_move as the test). */
 int oracle_solve_node(uint8_t *g)
 {
-    return solve_rec(g, oracle_is_valid_move);
+    return solve_rec(g, oracle_is_valid_move, node_order_cell);
 }
 
 uint64_t oracle_last_nodes(void) { return g_nodes; }
@@ -158,6 +189,14 @@ void oracle_solve_batch(const uint8_t *in, uint8_t *out, int32_t *status, int64_
     for (int64_t p = 0; p < n; p++) {
         memcpy(out + p * 81, in + p * 81, 81);
         status[p] = oracle_solve(out + p * 81);
+    }
+}
+
+void oracle_solve_batch_rowmajor(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n)
+{
+    for (int64_t p = 0; p < n; p++) {
+        memcpy(out + p * 81, in + p * 81, 81);
+        status[p] = oracle_solve_rowmajor(out + p * 81);
     }
 }
 
@@ -318,9 +357,7 @@ static double now_s(void)
 
 static int solve_rec_timed(uint8_t *g)
 {
-    int cell = -1;
-    for (int i = 0; i < 81; i++)
-        if (g[i] == 0) { cell = i; break; }
+    int cell = gen_order_cell(g);
     if (cell < 0) return 1;
     int row = cell / 9, col = cell % 9;
     for (int num = 1; num <= 9; num++) {

@@ -16,6 +16,9 @@ SDK_UNSOLVABLE = 0
 SDK_SOLVED = 1
 SDK_INVALID = -1
 SDK_CANCELLED = -2
+SDK_ORDER_GEN = 0    # gen.py:6-28's walk (last row with an empty cell first)
+SDK_ORDER_NODE = 1   # node.py:62-74's walk (row-major)
+ORDERS = {"gen": SDK_ORDER_GEN, "node": SDK_ORDER_NODE}
 
 # every symbol include/sudoku_hip.h declares
 EXPORTS = (
@@ -51,13 +54,13 @@ def load() -> ctypes.CDLL:
     L.sdk_workspace_bytes.restype = sz
     L.sdk_workspace_bytes.argtypes = []
     L.sdk_solve_batch.restype = i32
-    L.sdk_solve_batch.argtypes = [vp, vp, vp, i64, vp, i32, vp]
+    L.sdk_solve_batch.argtypes = [vp, vp, vp, i64, vp, i32, i32, vp]
     L.sdk_check_batch.restype = i32
     L.sdk_check_batch.argtypes = [vp, vp, i64, i32, vp]
     L.sdk_first_candidate_batch.restype = i32
     L.sdk_first_candidate_batch.argtypes = [vp, vp, vp, i64, vp]
     L.sdk_expand_frontier.restype = i32
-    L.sdk_expand_frontier.argtypes = [vp, i64, vp, vp, vp, i64, vp]
+    L.sdk_expand_frontier.argtypes = [vp, i64, vp, vp, vp, i64, i32, vp]
     L.sdk_read_stats.restype = i32
     L.sdk_read_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i32, vp]
     L.sdk_last_error.restype = ctypes.c_char_p
@@ -74,3 +77,14 @@ def check(rc: int, what: str) -> None:
     if rc != 0:
         msg = load().sdk_last_error().decode(errors="replace")
         raise SudokuHipError(f"{what} failed ({rc}): {msg}")
+
+
+def order_code(order) -> int:
+    """'gen' | 'node' | SDK_ORDER_* -> SDK_ORDER_*."""
+    if isinstance(order, str):
+        if order not in ORDERS:
+            raise ValueError(f"order must be one of {sorted(ORDERS)}")
+        return ORDERS[order]
+    if order not in (SDK_ORDER_GEN, SDK_ORDER_NODE):
+        raise ValueError(f"bad order {order!r}")
+    return int(order)

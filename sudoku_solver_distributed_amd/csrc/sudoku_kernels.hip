@@ -1,14 +1,20 @@
 // sudoku_kernels.hip -- MI355X (gfx950, CDNA4) Sudoku solver kernels + C ABI.
 //
 // Hot path: batch solving of 9x9 boards, bit-identical to the reference's
-// backtracking walk (gen.py:6-28 solve_sudoku; node.py:62-74
-// SudokuSolver.solve_sudoku_recursive): the walk fills the FIRST empty cell in
-// row-major order with digits 1..9 ascending, so its first solution is the
-// lexicographically smallest completion.  We reach the same board with far
-// fewer nodes by interleaving sound propagation (naked singles, hidden
-// singles, conflict detection) with branching on that same first empty cell
-// in the same digit order: propagation only removes completions, never
-// reorders them, so the first completion found is still the smallest one.
+// backtracking walks.  Both fill one cell at a time with digits 1..9
+// ascending; they differ in which empty cell they pick:
+//   SDK_ORDER_GEN  gen.py:6-28 solve_sudoku -- its scan (gen.py:11-15) breaks
+//                  only the column loop, so it takes the first empty cell of
+//                  the LAST row that has one (rows 8..0, columns 0..8);
+//   SDK_ORDER_NODE node.py:62-74 solve_sudoku_recursive -- first empty cell
+//                  in row-major order.
+// Either way the cell sequence is a fixed order of the empty cells, so the
+// walk's first solution is the lexicographically smallest completion in that
+// order.  We reach the same board with far fewer nodes by interleaving sound
+// propagation (naked singles, hidden singles, conflict detection) with
+// branching on the same first-in-order empty cell and the same digit order:
+// propagation only removes completions, never reorders them, so the first
+// completion found is still the smallest one.
 //
 // Execution model:
 //   * one 64-lane wavefront owns one board; lane l owns cell l (slot 0) and,
@@ -51,9 +57,9 @@ enum {
 };
 
 struct __attribute__((aligned(16))) WaveLds {
-    uint32_t M[28];  // unit masks of filled cells
-    uint32_t O[28];  // digits seen at least once among empty cells' candidates
-    uint32_t T[28];  // digits seen at least twice
+    uint32_t M[28];  // unit masks of filled cells (rows 0-8, columns 9-17, boxes 18-26)
+    uint32_t T[28];  // per unit: digits that are candidates of >= 2 of its empty cells
+    uint32_t C[84];  // per cell: candidate mask published for the unit gather (0 = filled)
     uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
     uint32_t pad[3];
 };
@@ -74,13 +80,16 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
-// Per-lane view of its two cells.
+// Per-lane view of its two cells, plus the lane's unit role (lanes 0..26).
 struct Cells {
     uint32_t v0, v1;    // digit 0..9 (0 = empty)
     uint32_t lv0, lv1;  // depth at which the cell was filled (givens: 0)
     bool g0, g1;        // given
+    bool nw0, nw1;      // placed since the last sweep: not yet in the unit masks
     int r0, c0, b0, r1, c1, b1;
     bool has1;
+    // unit gather: lane u < 27 reads the cells ub + k*us1 + (k/3)*us2, k = 0..8
+    int ub, us1, us2;
 };
 
 __device__ __forceinline__ void cell_units(int cell, int &r, int &c, int &b)
@@ -88,6 +97,16 @@ __device__ __forceinline__ void cell_units(int cell, int &r, int &c, int &b)
     r = cell / 9;
     c = cell - r * 9;
     b = (r / 3) * 3 + c / 3;
+}
+
+__device__ __forceinline__ void init_lane(Cells &s, int lane)
+{
+    cell_units(lane, s.r0, s.c0, s.b0);
+    cell_units(lane < 17 ? 64 + lane : 80, s.r1, s.c1, s.b1);
+    if (lane < 9) { s.ub = 9 * lane; s.us1 = 1; s.us2 = 0; }                      // row
+    else if (lane < 18) { s.ub = lane - 9; s.us1 = 9; s.us2 = 0; }                // column
+    else { const int b = lane < 27 ? lane - 18 : 0;                               // box
+           s.ub = (b / 3) * 27 + (b % 3) * 3; s.us1 = 1; s.us2 = 6; }
 }
 
 // Load one board (81 bytes) into the wave.  Returns false (wave-uniform) if
@@ -103,10 +122,13 @@ __device__ __forceinline__ bool load_board(const uint8_t *__restrict__ src, int 
     s.g1 = s.has1 && b != 0;
     s.lv0 = 0;
     s.lv1 = 0;
+    s.nw0 = false;
+    s.nw1 = false;
     return !__any(a > 9 || b > 9);
 }
 
-// Build the givens' unit masks (returned in lanes 0..26) and the bad-unit mask.
+// Build the givens' unit masks (returned in lanes 0..26; W.M holds them on
+// return) and the bad-unit mask.
 __device__ __forceinline__ uint32_t build_given_masks(WaveLds &W, int lane, const Cells &s, uint32_t &bad)
 {
     if (lane < 28) W.M[lane] = 0;
@@ -139,25 +161,44 @@ enum { PROP_OPEN = 0, PROP_DEAD = 1, PROP_SOLVED = 2 };
 // when no cell is empty, otherwise PROP_OPEN and sets `placed` if any single
 // was placed (then call again).  When it returns PROP_OPEN with !placed the
 // state is a fixpoint and cand0/cand1 hold every empty cell's candidates.
+//
+// Unit masks live in W.M across sweeps: normally only the cells placed since
+// the last sweep are OR-ed in (their returning atomics also catch two
+// placements of one digit in one unit); after a backtrack (`rebuild`) the
+// masks are rebuilt from the givens and every filled cell.
 __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gmask, uint32_t bad,
-                                     uint32_t depth, uint32_t &cand0, uint32_t &cand1, bool &placed)
+                                     uint32_t depth, bool &rebuild, uint32_t &cand0, uint32_t &cand1,
+                                     bool &placed)
 {
     placed = false;
-    // ---- phase A: unit masks of all filled cells; clash detection
-    if (lane < 27) W.M[lane] = gmask;
-    wave_lds_sync();
+    // ---- phase A: bring the unit masks up to date; clash detection
+    bool f0, f1;
+    if (rebuild) {
+        if (lane < 27) W.M[lane] = gmask;
+        f0 = s.v0 != 0 && !s.g0;
+        f1 = s.has1 && s.v1 != 0 && !s.g1;
+    } else {
+        f0 = s.nw0;
+        f1 = s.nw1;
+    }
+    s.nw0 = false;
+    s.nw1 = false;
     uint32_t clash = 0;
-    if (s.v0 != 0 && !s.g0) {
-        uint32_t bit = 1u << (s.v0 - 1);
-        clash |= (atomicOr(&W.M[s.r0], bit) | atomicOr(&W.M[9 + s.c0], bit) |
-                  atomicOr(&W.M[18 + s.b0], bit)) & bit;
+    if (rebuild || __any(f0 || f1)) {
+        wave_lds_sync();
+        if (f0) {
+            uint32_t bit = 1u << (s.v0 - 1);
+            clash |= (atomicOr(&W.M[s.r0], bit) | atomicOr(&W.M[9 + s.c0], bit) |
+                      atomicOr(&W.M[18 + s.b0], bit)) & bit;
+        }
+        if (f1) {
+            uint32_t bit = 1u << (s.v1 - 1);
+            clash |= (atomicOr(&W.M[s.r1], bit) | atomicOr(&W.M[9 + s.c1], bit) |
+                      atomicOr(&W.M[18 + s.b1], bit)) & bit;
+        }
+        wave_lds_sync();
     }
-    if (s.has1 && s.v1 != 0 && !s.g1) {
-        uint32_t bit = 1u << (s.v1 - 1);
-        clash |= (atomicOr(&W.M[s.r1], bit) | atomicOr(&W.M[9 + s.c1], bit) |
-                  atomicOr(&W.M[18 + s.b1], bit)) & bit;
-    }
-    wave_lds_sync();
+    rebuild = false;
     const bool e0 = s.v0 == 0;
     const bool e1 = s.has1 && s.v1 == 0;
     cand0 = e0 ? (~(W.M[s.r0] | W.M[9 + s.c0] | W.M[18 + s.b0]) & 0x1FFu) : 0u;
@@ -170,31 +211,31 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     const bool n0 = e0 && (cand0 & (cand0 - 1)) == 0;
     const bool n1 = e1 && (cand1 & (cand1 - 1)) == 0;
     if (__any(n0 || n1)) {
-        if (n0) { s.v0 = __builtin_ctz(cand0) + 1; s.lv0 = depth; }
-        if (n1) { s.v1 = __builtin_ctz(cand1) + 1; s.lv1 = depth; }
+        if (n0) { s.v0 = __builtin_ctz(cand0) + 1; s.lv0 = depth; s.nw0 = true; }
+        if (n1) { s.v1 = __builtin_ctz(cand1) + 1; s.lv1 = depth; s.nw1 = true; }
         placed = true;
         return PROP_OPEN;
     }
 
-    // ---- phase B: hidden singles and digits with no place in a unit
-    if (lane < 28) { W.O[lane] = 0; W.T[lane] = 0; }
-    wave_lds_sync();
-    if (e0) {
-        uint32_t o;
-        o = atomicOr(&W.O[s.r0], cand0);      atomicOr(&W.T[s.r0], o & cand0);
-        o = atomicOr(&W.O[9 + s.c0], cand0);  atomicOr(&W.T[9 + s.c0], o & cand0);
-        o = atomicOr(&W.O[18 + s.b0], cand0); atomicOr(&W.T[18 + s.b0], o & cand0);
-    }
-    if (e1) {
-        uint32_t o;
-        o = atomicOr(&W.O[s.r1], cand1);      atomicOr(&W.T[s.r1], o & cand1);
-        o = atomicOr(&W.O[9 + s.c1], cand1);  atomicOr(&W.T[9 + s.c1], o & cand1);
-        o = atomicOr(&W.O[18 + s.b1], cand1); atomicOr(&W.T[18 + s.b1], o & cand1);
-    }
+    // ---- phase B: hidden singles and digits with no place in a unit.
+    // Cells publish their candidates; lanes 0..26 each gather one unit's nine
+    // cells (conflict-light plain reads) and fold "seen once / seen twice".
+    W.C[lane] = cand0;
+    if (s.has1) W.C[64 + lane] = cand1;
     wave_lds_sync();
     bool udead = false;
-    if (lane < 27 && !((bad >> lane) & 1u))
-        udead = (W.O[lane] | W.M[lane]) != 0x1FFu;
+    if (lane < 27) {
+        uint32_t once = 0, twice = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint32_t x = W.C[s.ub + k * s.us1 + (k / 3) * s.us2];
+            twice |= once & x;
+            once |= x;
+        }
+        W.T[lane] = twice;
+        if (!((bad >> lane) & 1u)) udead = (once | W.M[lane]) != 0x1FFu;
+    }
+    wave_lds_sync();
     uint32_t h0 = 0, h1 = 0;
     if (e0) {
         if (!((bad >> s.r0) & 1u)) h0 |= cand0 & ~W.T[s.r0];
@@ -209,46 +250,56 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     const bool dead2 = udead || (h0 & (h0 - 1)) != 0 || (h1 & (h1 - 1)) != 0;
     if (__any(dead2)) return PROP_DEAD;
     if (__any(h0 != 0 || h1 != 0)) {
-        if (h0) { s.v0 = __builtin_ctz(h0) + 1; s.lv0 = depth; }
-        if (h1) { s.v1 = __builtin_ctz(h1) + 1; s.lv1 = depth; }
+        if (h0) { s.v0 = __builtin_ctz(h0) + 1; s.lv0 = depth; s.nw0 = true; }
+        if (h1) { s.v1 = __builtin_ctz(h1) + 1; s.lv1 = depth; s.nw1 = true; }
         placed = true;
     }
     return PROP_OPEN;
 }
 
 __device__ __forceinline__ int propagate(WaveLds &W, int lane, Cells &s, uint32_t gmask, uint32_t bad,
-                                         uint32_t depth, uint32_t &cand0, uint32_t &cand1, uint32_t &sweeps)
+                                         uint32_t depth, bool &rebuild, uint32_t &cand0, uint32_t &cand1,
+                                         uint32_t &sweeps)
 {
     for (;;) {
         bool placed;
-        int st = sweep(W, lane, s, gmask, bad, depth, cand0, cand1, placed);
+        int st = sweep(W, lane, s, gmask, bad, depth, rebuild, cand0, cand1, placed);
         sweeps++;
         if (st != PROP_OPEN || !placed) return st;
     }
 }
 
-// first empty cell (row-major) and its candidates; requires a fixpoint state
-__device__ __forceinline__ void first_empty(const Cells &s, uint32_t cand0, uint32_t cand1, int &cell, uint32_t &cand)
+// The walk's next cell among the empty cells {eb0 (cells 0..63), eb1 (64..80)},
+// not both zero.  Scalar bit work only.
+__device__ __forceinline__ int order_cell(uint64_t eb0, uint64_t eb1, int order)
+{
+    if (order == SDK_ORDER_NODE)  // node.py:63-65: row-major first
+        return eb0 ? __builtin_ctzll(eb0) : 64 + __builtin_ctzll(eb1);
+    // gen.py:11-15: last row holding an empty cell, its first empty column
+    const int hi = eb1 ? 64 + 63 - __builtin_clzll(eb1) : 63 - __builtin_clzll(eb0);
+    const int start = (hi / 9) * 9;
+    if (start >= 64) return start + __builtin_ctzll(eb1 >> (start - 64));
+    const uint64_t m = eb0 & (~0ull << start);
+    return m ? __builtin_ctzll(m) : 64 + __builtin_ctzll(eb1);
+}
+
+// the walk's branch cell and its candidates; requires a fixpoint state
+__device__ __forceinline__ void first_empty(const Cells &s, uint32_t cand0, uint32_t cand1, int order, int &cell,
+                                            uint32_t &cand)
 {
     const uint64_t eb0 = __ballot(s.v0 == 0);
-    if (eb0) {
-        cell = __builtin_ctzll(eb0);
-        cand = rdlane(cand0, cell);
-    } else {
-        const uint64_t eb1 = __ballot(s.has1 && s.v1 == 0);
-        const int l = __builtin_ctzll(eb1);
-        cell = 64 + l;
-        cand = rdlane(cand1, l);
-    }
+    const uint64_t eb1 = __ballot(s.has1 && s.v1 == 0);
+    cell = order_cell(eb0, eb1, order);
+    cand = cell < 64 ? rdlane(cand0, cell) : rdlane(cand1, cell - 64);
 }
 
 __device__ __forceinline__ void place(Cells &s, int lane, int cell, uint32_t dbit, uint32_t level)
 {
     const uint32_t v = __builtin_ctz(dbit) + 1;
     if (cell < 64) {
-        if (lane == cell) { s.v0 = v; s.lv0 = level; }
+        if (lane == cell) { s.v0 = v; s.lv0 = level; s.nw0 = true; }
     } else {
-        if (lane == cell - 64) { s.v1 = v; s.lv1 = level; }
+        if (lane == cell - 64) { s.v1 = v; s.lv1 = level; s.nw1 = true; }
     }
 }
 
@@ -262,22 +313,24 @@ __device__ __forceinline__ void store_board(uint8_t *__restrict__ dst, int lane,
 
 // Full search of one board.  Returns SDK_SOLVED / SDK_UNSOLVABLE /
 // SDK_CANCELLED; on SOLVED the cells hold the walk's first solution.
-__device__ __forceinline__ int search(WaveLds &W, int lane, Cells &s, int64_t idx,
+__device__ __forceinline__ int search(WaveLds &W, int lane, Cells &s, int64_t idx, int order,
                                       const int64_t *best, uint32_t &guesses, uint32_t &sweeps)
 {
     uint32_t bad;
     const uint32_t gmask = build_given_masks(W, lane, s, bad);
+    bool rebuild = false;  // W.M already holds exactly the givens
     uint32_t depth = 0;
     uint32_t stk0 = 0, stk1 = 0;  // DFS stack: level k lives in lane k&63 of stk(k>>6)
     uint32_t cand0, cand1;
     for (;;) {
-        int st = propagate(W, lane, s, gmask, bad, depth, cand0, cand1, sweeps);
+        int st = propagate(W, lane, s, gmask, bad, depth, rebuild, cand0, cand1, sweeps);
         if (st == PROP_SOLVED) return SDK_SOLVED;
         if (st == PROP_OPEN) {
-            // branch on the first empty cell, smallest digit first
+            // branch on the walk's next cell, smallest digit first
             int cell;
             uint32_t cand;
-            first_empty(s, cand0, cand1, cell, cand);
+            first_empty(s, cand0, cand1, order, cell, cand);
+            if (cand == 0) return SDK_FAULT;  // unreachable: a fixpoint has no empty cell without candidates
             const uint32_t d = lowbit(cand);
             const uint32_t entry = ((uint32_t)cell << 9) | (cand ^ d);
             if (depth < 64) { if (lane == (int)depth) stk0 = entry; }
@@ -292,6 +345,9 @@ __device__ __forceinline__ int search(WaveLds &W, int lane, Cells &s, int64_t id
             continue;
         }
         // dead: backtrack to the deepest level with an untried digit
+        rebuild = true;
+        s.nw0 = false;
+        s.nw1 = false;
         for (;;) {
             if (depth == 0) return SDK_UNSOLVABLE;
             const uint32_t top = depth - 1;
@@ -324,7 +380,7 @@ __global__ void arm_kernel(unsigned long long *ws)
 
 __global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
-    int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered)
+    int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered, int order)
 {
     __shared__ WaveLds lds[WAVES_PER_BLOCK];
     const int lane = threadIdx.x & 63;
@@ -341,8 +397,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
         const int64_t end = base + chunk < n ? base + chunk : n;
         for (int64_t p = base; p < end; ++p) {
             Cells s;
-            cell_units(lane, s.r0, s.c0, s.b0);
-            cell_units(lane < 17 ? 64 + lane : 80, s.r1, s.c1, s.b1);
+            init_lane(s, lane);
             const uint8_t *src = puzzles + p * 81;
             uint8_t *dst = sols + p * 81;
             int st;
@@ -354,7 +409,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
                 st = SDK_CANCELLED;
                 store_board(dst, lane, s, true);
             } else {
-                st = search(W, lane, s, p, best, guesses, sweeps);
+                st = search(W, lane, s, p, order, best, guesses, sweeps);
                 store_board(dst, lane, s, st != SDK_SOLVED);
                 if (st == SDK_SOLVED) {
                     solved++;
@@ -462,7 +517,7 @@ __global__ __launch_bounds__(256) void first_candidate_kernel(const uint8_t *__r
 // the number of children it will produce.
 __global__ __launch_bounds__(BLOCK_THREADS) void expand_count_kernel(const uint8_t *__restrict__ nodes, int64_t n,
                                                                      uint8_t *__restrict__ tmp,
-                                                                     int64_t *__restrict__ counts)
+                                                                     int64_t *__restrict__ counts, int order)
 {
     __shared__ WaveLds lds[WAVES_PER_BLOCK];
     const int lane = threadIdx.x & 63;
@@ -470,21 +525,21 @@ __global__ __launch_bounds__(BLOCK_THREADS) void expand_count_kernel(const uint8
     const int64_t p = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
     if (p >= n) return;
     Cells s;
-    cell_units(lane, s.r0, s.c0, s.b0);
-    cell_units(lane < 17 ? 64 + lane : 80, s.r1, s.c1, s.b1);
+    init_lane(s, lane);
     uint8_t *dst = tmp + p * 81;
     int64_t cnt = 0;
     if (load_board(nodes + p * 81, lane, s)) {
         uint32_t bad;
         const uint32_t gmask = build_given_masks(W, lane, s, bad);
         uint32_t cand0, cand1, sweeps = 0;
-        const int st = propagate(W, lane, s, gmask, bad, 0, cand0, cand1, sweeps);
+        bool rebuild = false;
+        const int st = propagate(W, lane, s, gmask, bad, 0, rebuild, cand0, cand1, sweeps);
         if (st == PROP_SOLVED) {
             cnt = 1;
         } else if (st == PROP_OPEN) {
             int cell;
             uint32_t cand;
-            first_empty(s, cand0, cand1, cell, cand);
+            first_empty(s, cand0, cand1, order, cell, cand);
             cnt = __builtin_popcount(cand);
         }
     }
@@ -521,7 +576,8 @@ __global__ __launch_bounds__(1024) void scan_kernel(const int64_t *__restrict__ 
 // pass 2: write children (one wave per node) in digit order
 __global__ __launch_bounds__(BLOCK_THREADS) void expand_write_kernel(const uint8_t *__restrict__ tmp, int64_t n,
                                                                      const int64_t *__restrict__ offsets,
-                                                                     uint8_t *__restrict__ children, int64_t cap)
+                                                                     uint8_t *__restrict__ children, int64_t cap,
+                                                                     int order)
 {
     const int lane = threadIdx.x & 63;
     const int64_t p = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
@@ -534,7 +590,7 @@ __global__ __launch_bounds__(BLOCK_THREADS) void expand_write_kernel(const uint8
     // candidates of the first empty cell recomputed from the grid itself
     const uint64_t eb0 = __ballot(a == 0);
     const uint64_t eb1 = __ballot(lane < 17 && b == 0);
-    int cell = eb0 ? __builtin_ctzll(eb0) : (eb1 ? 64 + __builtin_ctzll(eb1) : -1);
+    const int cell = (eb0 | eb1) ? order_cell(eb0, eb1, order) : -1;
     uint32_t used = 0;
     if (cell >= 0) {
         const int r = cell / 9, c = cell % 9, br = (r / 3) * 3, bc = (c / 3) * 3;
@@ -593,14 +649,15 @@ static int cu_count()
 extern "C" {
 
 const char *sdk_last_error(void) { return g_err; }
-const char *sdk_version(void) { return "sudoku_hip 0.1 gfx950 wave-per-board lex-order"; }
+const char *sdk_version(void) { return "sudoku_hip 0.1 gfx950 wave-per-board walk-order"; }
 int sdk_device_cu_count(void) { return cu_count(); }
 size_t sdk_workspace_bytes(void) { return WS_WORDS * sizeof(unsigned long long); }
 
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
-                    void *d_workspace, int ordered, void *stream)
+                    void *d_workspace, int order, int ordered, void *stream)
 {
-    if (n < 0 || (n > 0 && (!d_puzzles || !d_solutions || !d_status || !d_workspace))) {
+    if (n < 0 || (n > 0 && (!d_puzzles || !d_solutions || !d_status || !d_workspace)) ||
+        (order != SDK_ORDER_GEN && order != SDK_ORDER_NODE)) {
         snprintf(g_err, sizeof g_err, "sdk_solve_batch: bad arguments (n=%lld)", (long long)n);
         return -2;
     }
@@ -617,7 +674,7 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     if (chunk > 16) chunk = 16;
     const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
     hipLaunchKernelGGL(solve_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
-                       d_status, n, ws, chunk, ordered);
+                       d_status, n, ws, chunk, ordered, order);
     e = hipGetLastError();
     if (e != hipSuccess) return set_err("sdk_solve_batch: launch", e);
     return 0;
@@ -651,9 +708,10 @@ int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells, in
 }
 
 int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64_t *d_offsets,
-                        uint8_t *d_children, int64_t cap, void *stream)
+                        uint8_t *d_children, int64_t cap, int order, void *stream)
 {
-    if (n < 0 || cap < 0 || (n > 0 && (!d_nodes || !d_tmp || !d_offsets || (cap > 0 && !d_children)))) {
+    if (n < 0 || cap < 0 || (n > 0 && (!d_nodes || !d_tmp || !d_offsets || (cap > 0 && !d_children))) ||
+        (order != SDK_ORDER_GEN && order != SDK_ORDER_NODE)) {
         snprintf(g_err, sizeof g_err, "sdk_expand_frontier: bad arguments");
         return -2;
     }
@@ -664,10 +722,11 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
     }
     const unsigned blocks = (unsigned)((n + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK);
     // per-node child counts are written into d_offsets[0..n) and scanned in place
-    hipLaunchKernelGGL(expand_count_kernel, dim3(blocks), dim3(BLOCK_THREADS), 0, st, d_nodes, n, d_tmp, d_offsets);
+    hipLaunchKernelGGL(expand_count_kernel, dim3(blocks), dim3(BLOCK_THREADS), 0, st, d_nodes, n, d_tmp, d_offsets,
+                       order);
     hipLaunchKernelGGL(scan_kernel, dim3(1), dim3(1024), 0, st, d_offsets, d_offsets, n);
     hipLaunchKernelGGL(expand_write_kernel, dim3(blocks), dim3(BLOCK_THREADS), 0, st, d_tmp, n, d_offsets,
-                       d_children, cap);
+                       d_children, cap, order);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_err("sdk_expand_frontier: launch", e);
 }

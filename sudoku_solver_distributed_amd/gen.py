@@ -37,6 +37,9 @@ SEEDS_17 = (
     "000000000000003085001020000000507000004000100090000000500000073002010000000040009",
 )
 PATHOLOGICAL = SEEDS_17[5]
+# a 21-clue unique board that naked + hidden singles cannot finish: needs
+# real search under either walk order (frontier-split tests / latency bench)
+SEARCH_HEAVY = "800000000003600000070090200050007000000045700000100030001000068008500010090000400"
 
 
 def _board_from_flat(flat) -> List[List[int]]:

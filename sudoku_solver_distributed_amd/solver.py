@@ -87,9 +87,10 @@ class BatchSolver:
 
     # -------------------------------------------------------------- solve
     def solve(self, puzzles, out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
-              ordered: bool = False, stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
-        """Solve every board (gen.py:6-28 semantics).  Asynchronous on the
-        stream; returns (solutions uint8 (n,81), status int32 (n,))."""
+              ordered: bool = False, order="gen", stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Solve every board with the reference walk `order` ("gen":
+        gen.py:6-28, "node": node.py:62-74).  Asynchronous on the stream;
+        returns (solutions uint8 (n,81), status int32 (n,))."""
         p = self._dev(as_boards(puzzles))
         n = p.shape[0]
         if out is None:
@@ -102,8 +103,8 @@ class BatchSolver:
             raise ValueError("status must be an (n,) int32 tensor")
         with torch.cuda.device(self.device):
             rc = self.lib.sdk_solve_batch(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
-                                          self.workspace.data_ptr(), 1 if ordered else 0,
-                                          self._stream(stream))
+                                          self.workspace.data_ptr(), _lib.order_code(order),
+                                          1 if ordered else 0, self._stream(stream))
         _lib.check(rc, "sdk_solve_batch")
         return out, status
 
@@ -129,7 +130,7 @@ class BatchSolver:
         _lib.check(rc, "sdk_first_candidate_batch")
         return num
 
-    def expand(self, nodes, stream=None) -> torch.Tensor:
+    def expand(self, nodes, order="gen", stream=None) -> torch.Tensor:
         """One frontier level (sdk_expand_frontier); synchronises to size it."""
         nd = self._dev(as_boards(nodes))
         n = nd.shape[0]
@@ -139,7 +140,8 @@ class BatchSolver:
         children = torch.empty((max(cap, 1), 81), dtype=torch.uint8, device=self.device)
         with torch.cuda.device(self.device):
             rc = self.lib.sdk_expand_frontier(nd.data_ptr(), n, tmp.data_ptr(), offsets.data_ptr(),
-                                              children.data_ptr(), cap, self._stream(stream))
+                                              children.data_ptr(), cap, _lib.order_code(order),
+                                              self._stream(stream))
         _lib.check(rc, "sdk_expand_frontier")
         total = int(offsets[n].item()) if n else 0
         if total > cap:
@@ -154,29 +156,33 @@ class BatchSolver:
         return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4]}
 
     # ------------------------------------------------------ frontier split
-    def frontier(self, board, target: int = 4096, max_levels: int = 81) -> torch.Tensor:
-        """Expand one board's search tree (in the walk's order) until the
-        frontier holds >= target nodes or cannot grow."""
+    def frontier(self, board, target: int = 4096, max_levels: int = 81, order="gen") -> torch.Tensor:
+        """Expand one board's search tree level by level (in the walk's
+        order) until the frontier holds >= target nodes, or the next level
+        would be narrower (dead branches outnumber new ones), or nothing is
+        left to split.  Returns the frontier, in walk order."""
         nodes = self._dev(as_boards(board))
         for _ in range(max_levels):
             if nodes.shape[0] >= target or nodes.shape[0] == 0:
                 break
-            children = self.expand(nodes)
+            children = self.expand(nodes, order=order)
             if children.shape[0] == nodes.shape[0] and torch.equal(children, nodes):
                 break  # every node already solved: nothing left to split
+            if 0 < children.shape[0] < nodes.shape[0]:
+                break  # narrowing: keep the wider level
             nodes = children
         return nodes
 
-    def solve_one_split(self, board, target: int = 4096) -> Tuple[bool, torch.Tensor]:
+    def solve_one_split(self, board, target: int = 4096, order="gen") -> Tuple[bool, torch.Tensor]:
         """Single hard board: frontier split over all waves of this GPU, then
         an ordered solve; returns (solved, grid81)."""
         root = self._dev(as_boards(board))
         if root.shape[0] != 1:
             raise ValueError("solve_one_split takes exactly one board")
-        nodes = self.frontier(root, target)
+        nodes = self.frontier(root, target, order=order)
         if nodes.shape[0] == 0:
             return False, root[0].clone()
-        sols, st = self.solve(nodes, ordered=True)
+        sols, st = self.solve(nodes, ordered=True, order=order)
         hit = torch.nonzero(st == SDK_SOLVED)
         if hit.numel() == 0:
             return False, root[0].clone()

@@ -43,12 +43,13 @@ def test_golden_named(solver):
         assert _s(sols[0].cpu()) == c["solution"], c["name"]
 
 
-def test_random_generated_vs_oracle(solver):
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_random_generated_vs_oracle(solver, order):
     from sudoku_solver_distributed_amd.gen import generate_batch
     for empties, n in ((30, 256), (50, 256), (58, 256), (64, 128), (70, 64), (81, 4)):
         puzzles = generate_batch(n, empties, seed=1234 + empties)
-        sols, st = solver.solve(puzzles)
-        want, wst = O.solve_batch(puzzles.cpu().numpy())
+        sols, st = solver.solve(puzzles, order=order)
+        want, wst = O.solve_batch(puzzles.cpu().numpy(), order=order)
         assert np.array_equal(st.cpu().numpy(), wst), empties
         assert np.array_equal(sols.cpu().numpy(), want), empties
 
@@ -83,28 +84,38 @@ def test_hard17_vs_unique_oracle(solver):
 
 
 def test_seeds_vs_literal_walk(solver):
-    """Every 17-clue seed against the literal walk (oracle_solve, seconds each)."""
+    """17-clue seeds against the literal row-major walk (seconds each)."""
     from sudoku_solver_distributed_amd.gen import SEEDS_17
     p = np.array([b81(s) for s in SEEDS_17], dtype=np.uint8)
-    sols, st = solver.solve(torch.from_numpy(p))
-    want, wst = O.solve_batch(p)
+    sols, st = solver.solve(torch.from_numpy(p), order="node")
+    want, wst = O.solve_batch(p, order="node")
     assert np.array_equal(sols.cpu().numpy(), want)
     assert np.array_equal(st.cpu().numpy(), wst)
 
 
-def test_edge_cases(solver):
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_edge_cases(solver, order):
     full = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
     bad_full = "5" * 81
     dead = "123456780000000009" + "0" * 63
-    dup = "550000000" + "0" * 72
-    boards = [full, bad_full, dead, dup, "0" * 81]
+    # clash in row 0 (cells 0 and 1 both 8) plus three blanks: completable
+    dup = "88" + full[2:30] + "0" + full[31:50] + "0" + full[51:70] + "0" + full[71:]
+    boards = [full, bad_full, dup, "0" * 81, dead]
     p = np.array([b81(s) for s in boards], dtype=np.uint8)
-    sols, st = solver.solve(torch.from_numpy(p))
-    want, wst = O.solve_batch(p)
-    assert np.array_equal(st.cpu().numpy(), wst)
-    assert np.array_equal(sols.cpu().numpy(), want)
+    sols, st = solver.solve(torch.from_numpy(p), order=order)
+    sols, st = sols.cpu().numpy(), st.cpu().numpy()
+    # the literal walk is tractable on all but `dead` in gen order (it would
+    # enumerate rows 8..1 before reaching the dead cell in row 0)
+    k = len(boards) if order == "node" else len(boards) - 1
+    want, wst = O.solve_batch(p[:k], order=order)
+    assert np.array_equal(st[:k], wst)
+    assert np.array_equal(sols[:k], want)
+    # `dead` has no completion (counter), so the walk's verdict is False and
+    # the board is returned unchanged
+    assert O.count_solutions(p[4], 1) == 0 and O.count_solutions(p[2], 1) >= 1
+    assert st[4] == 0 and np.array_equal(sols[4], p[4])
     # empty batch
-    s0, t0 = solver.solve(torch.empty((0, 81), dtype=torch.uint8))
+    s0, t0 = solver.solve(torch.empty((0, 81), dtype=torch.uint8), order=order)
     assert s0.shape == (0, 81) and t0.shape == (0,)
 
 
@@ -120,20 +131,31 @@ def test_invalid_bytes_rejected(solver):
     assert int(sols[1, 5]) == 12
 
 
-def test_duplicate_givens_vs_oracle(solver):
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_duplicate_givens_vs_oracle(solver, order):
+    """Clashing givens: the walk never tests givens, so such boards can still
+    be completed (e.g. nearly full boards); compare where a completion exists
+    and the board is otherwise unchanged-False."""
     rng = np.random.default_rng(3)
     from sudoku_solver_distributed_amd.gen import generate_batch
-    base = generate_batch(200, 55, seed=77).cpu().numpy()
-    # inject one clashing given into each board
-    for b in base:
+    full = generate_batch(300, 0, seed=77).cpu().numpy()
+    base = full.copy()
+    for k, b in enumerate(base):
+        b[rng.choice(81, (5, 10, 20)[k % 3], replace=False)] = 0
         i, j = rng.choice(81, 2, replace=False)
         if b[i] == 0:
             b[i] = rng.integers(1, 10)
         b[j] = b[i]
-    sols, st = solver.solve(torch.from_numpy(base))
-    want, wst = O.solve_batch(base)
-    assert np.array_equal(st.cpu().numpy(), wst)
-    assert np.array_equal(sols.cpu().numpy(), want)
+    sols, st = solver.solve(torch.from_numpy(base), order=order)
+    sols, st = sols.cpu().numpy(), st.cpu().numpy()
+    cnt = np.array([O.count_solutions(b, 1) for b in base])
+    dead = cnt == 0
+    assert (st[dead] == 0).all() and np.array_equal(sols[dead], base[dead])
+    live = np.nonzero(~dead)[0]
+    assert live.size > 100
+    want, wst = O.solve_batch(base[live], order=order)
+    assert np.array_equal(st[live], wst)
+    assert np.array_equal(sols[live], want)
 
 
 def test_check_batch(solver):
@@ -153,18 +175,25 @@ def test_first_candidate(solver):
     assert got == [c["num"] or 0 for c in cases]
 
 
-def test_frontier_order_and_split(solver):
-    from sudoku_solver_distributed_amd.gen import PATHOLOGICAL
-    root = torch.tensor([b81(PATHOLOGICAL)], dtype=torch.uint8)
-    nodes = solver.frontier(root, target=512)
+# cell sequence of each walk (gen.py scans rows 8..0 in effect; node.py 0..8)
+WALK = {"gen": [r * 9 + c for r in range(8, -1, -1) for c in range(9)],
+        "node": list(range(81))}
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_frontier_order_and_split(solver, order):
+    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY
+    root = torch.tensor([b81(SEARCH_HEAVY)], dtype=torch.uint8)
+    nodes = solver.frontier(root, target=512, order=order)
     assert nodes.shape[0] >= 64
     # frontier nodes are in the walk's order: lexicographically increasing
-    a = nodes.cpu().numpy()
+    # along the walk's cell sequence
+    a = nodes.cpu().numpy()[:, WALK[order]]
     for i in range(a.shape[0] - 1):
         d = np.nonzero(a[i] != a[i + 1])[0]
         assert d.size and 0 < a[i, d[0]] < a[i + 1, d[0]]
-    ok, grid = solver.solve_one_split(root, target=2048)
-    want, cnt = O.solve_unique_batch(np.array([b81(PATHOLOGICAL)], dtype=np.uint8))
+    ok, grid = solver.solve_one_split(root, target=2048, order=order)
+    want, cnt = O.solve_unique_batch(np.array([b81(SEARCH_HEAVY)], dtype=np.uint8))
     assert ok and cnt[0] == 1
     assert np.array_equal(grid.cpu().numpy(), want[0])
 
