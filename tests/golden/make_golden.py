@@ -73,11 +73,14 @@ NAMED = {
     "full_fives": "5" * 81,
     # clashing givens (two 8s in row 0) with three blanks: still completable,
     # the walk never tests givens
-    "clash_completable": "88" + "7124635531679284642385179154" + "0" + "293867289716453376" + "0"
-                         + "5891292386754176594132" + "0" + "418532796",
+    "clash_completable": None,  # built below from full_valid
     # the walk's first cell (row 8 col 8) has no candidate: False at once
     "dead_first": "0" * 71 + "9" + "123456780",
 }
+_FULL = NAMED["full_valid"]
+NAMED["clash_completable"] = ("88" + _FULL[2:30] + "0" + _FULL[31:50] + "0" + _FULL[51:70] + "0"
+                              + _FULL[71:])
+assert all(len(v) == 81 for v in NAMED.values())
 
 def main(ref_dir, stages):
     sys.path.insert(0, ref_dir)
@@ -115,7 +118,14 @@ def main(ref_dir, stages):
 
     # -------------------------------------------------------------- solve
     solve_cases = []
+    only = os.environ.get("GOLDEN_ONLY")  # comma list: recompute these, keep the rest
+    solve_path = os.path.join(HERE, "golden_solve.json")
+    if only and os.path.exists(solve_path):
+        with open(solve_path) as f:
+            solve_cases = [c for c in json.load(f) if c["name"] not in only.split(",")]
     for name, p in (NAMED.items() if "solve" in stages else ()):
+        if only and name not in only.split(","):
+            continue
         board = b81(p)
         try:
             ok = run_limited(lambda: gen.solve_sudoku(board), 600)
@@ -126,7 +136,9 @@ def main(ref_dir, stages):
                             "solution": s81(board)})
         print("solve", name, ok, flush=True)
     if "solve" in stages:
-        with open(os.path.join(HERE, "golden_solve.json"), "w") as f:
+        order = {k: i for i, k in enumerate(NAMED)}
+        solve_cases.sort(key=lambda c: order.get(c["name"], 99))
+        with open(solve_path, "w") as f:
             json.dump(solve_cases, f, indent=0)
 
     # -------------------------------------------------------------- check
