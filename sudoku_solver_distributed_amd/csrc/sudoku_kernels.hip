@@ -646,6 +646,19 @@ static int cu_count()
     return g_cu_count[dev];
 }
 
+static int solve_blocks_per_cu()
+{
+    static std::atomic<int> cached{0};
+    int v = cached.load();
+    if (v) return v;
+    int nb = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, solve_kernel, BLOCK_THREADS, 0) != hipSuccess || nb <= 0)
+        nb = 4;
+    if (nb > 8) nb = 8;
+    cached.store(nb);
+    return nb;
+}
+
 extern "C" {
 
 const char *sdk_last_error(void) { return g_err; }
@@ -666,8 +679,8 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     unsigned long long *ws = (unsigned long long *)d_workspace;
     hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     hipError_t e;
-    // persistent grid: up to 8 waves per SIMD (32 per CU)
-    const int64_t max_waves = (int64_t)cu_count() * 32;
+    // persistent grid: exactly the resident waves (occupancy query, cached)
+    const int64_t max_waves = (int64_t)cu_count() * solve_blocks_per_cu() * WAVES_PER_BLOCK;
     int64_t waves = n < max_waves ? n : max_waves;
     int64_t chunk = n / (waves * 16);
     if (chunk < 1) chunk = 1;
