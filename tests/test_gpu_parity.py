@@ -235,3 +235,20 @@ def test_sudoku_class_api(solver):
     assert Sudoku(board).check() is True
     board[0][0], board[0][1] = board[0][1], board[0][0]
     assert Sudoku(board).check() is False
+
+
+def test_distributed_single_rank_gpu(solver):
+    """distributed.py on the product backend (HIP kernels), world of one."""
+    from sudoku_solver_distributed_amd.distributed import solve_shard, solve_split
+    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, hard17_batch
+    want, cnt = O.solve_unique_batch(np.array([b81(SEARCH_HEAVY)], dtype=np.uint8))
+    for order in ("gen", "node"):
+        st = {}
+        ok, grid = solve_split(torch.tensor([b81(SEARCH_HEAVY)], dtype=torch.uint8), order=order,
+                               target=256, chunk=16, stats=st)
+        assert ok and np.array_equal(grid.cpu().numpy(), want[0]), st
+    b = hard17_batch(1000, seed=9)
+    (lo, hi), sols, sts = solve_shard(b)
+    assert (lo, hi) == (0, 1000) and bool((sts == 1).all())
+    w, c = O.solve_unique_batch(b.numpy())
+    assert np.array_equal(sols.cpu().numpy(), w)
