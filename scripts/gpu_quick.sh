@@ -1,0 +1,10 @@
+#!/bin/bash
+# quick perf check: parity subset + bench at the full batch (twice)
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 150 --timeout-method thread -m gpu \
+  -k "golden_gen or random_generated or hard17_vs or edge_cases or duplicate or frontier or ordered" > gpurun_out/tq.log 2>&1
+rc=$?; tail -2 gpurun_out/tq.log; [ $rc -ne 0 ] && exit $rc
+for i in 1 2; do
+  timeout -k 10 120 python -u bench.py --steps 5 --batch 1048576 --no-cpu --latency-boards 8 > gpurun_out/bq.log 2>&1 || exit $?
+  python -c "import json;d=json.loads(open('gpurun_out/bq.log').read().strip().splitlines()[-1]);print(round(d['value']/1e6,1),'M/s', round(d['ms_per_step'],3),'ms p50', round(d['p50_single_ms'],4), 'sweeps', round(d['sweeps_per_board'],2))"
+done

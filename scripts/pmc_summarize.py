@@ -26,9 +26,11 @@ def load(d):
 
 def main():
     out, batch, seed, dirs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4:]
+    kernel = os.environ.get("PMC_KERNEL", "")
     vals = defaultdict(list)
     for d in dirs:
-        rows = [r for r in load(d) if r.get("Kernel_Name", "").startswith("solve_kernel")]
+        rows = [r for r in load(d) if r.get("Kernel_Name", "").split("(")[0] in
+                ((kernel,) if kernel else ("solve_kernel", "solve2_kernel"))]
         if not rows:
             continue
         gmax = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
@@ -40,7 +42,9 @@ def main():
         for (disp, name), v in per.items():
             vals[name].append(v)
     summary = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"kernel": "solve_kernel", "batch": batch, "seed": seed,
+    names = sorted({r.get("Kernel_Name", "").split("(")[0] for d in dirs for r in load(d)
+                    if r.get("Kernel_Name", "").startswith("solve")})
+    res = {"kernel": ",".join(names), "batch": batch, "seed": seed,
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),
            "hbm_bytes_per_launch": None}

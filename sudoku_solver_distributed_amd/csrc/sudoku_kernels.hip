@@ -37,6 +37,7 @@
 #include <stdio.h>
 #include <atomic>
 #include <mutex>
+#include <stdlib.h>
 
 #include "../../include/sudoku_hip.h"
 
@@ -59,7 +60,7 @@ enum {
 struct __attribute__((aligned(16))) WaveLds {
     uint32_t M[28];  // unit masks of filled cells (rows 0-8, columns 9-17, boxes 18-26)
     uint32_t T[28];  // per unit: digits that are candidates of >= 2 of its empty cells
-    uint32_t C[84];  // per cell: candidate mask published for the unit gather (0 = filled)
+    uint32_t C[128]; // per cell: candidate mask published for the unit gather (0 = filled; 81.. padding)
     uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
     uint32_t pad[3];
 };
@@ -201,8 +202,12 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     rebuild = false;
     const bool e0 = s.v0 == 0;
     const bool e1 = s.has1 && s.v1 == 0;
-    cand0 = e0 ? (~(W.M[s.r0] | W.M[9 + s.c0] | W.M[18 + s.b0]) & 0x1FFu) : 0u;
-    cand1 = e1 ? (~(W.M[s.r1] | W.M[9 + s.c1] | W.M[18 + s.b1]) & 0x1FFu) : 0u;
+    // unconditional reads + selects (lanes >= 17 address cell 80's units):
+    // no exec-mask branches around the loads
+    const uint32_t m0 = W.M[s.r0] | W.M[9 + s.c0] | W.M[18 + s.b0];
+    const uint32_t m1 = W.M[s.r1] | W.M[9 + s.c1] | W.M[18 + s.b1];
+    cand0 = e0 ? (~m0 & 0x1FFu) : 0u;
+    cand1 = e1 ? (~m1 & 0x1FFu) : 0u;
     const bool dead = clash != 0 || (e0 && cand0 == 0) || (e1 && cand1 == 0);
     if (__any(dead)) return PROP_DEAD;
     if (!__any(e0 || e1)) return PROP_SOLVED;
@@ -211,8 +216,12 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     const bool n0 = e0 && (cand0 & (cand0 - 1)) == 0;
     const bool n1 = e1 && (cand1 & (cand1 - 1)) == 0;
     if (__any(n0 || n1)) {
-        if (n0) { s.v0 = __builtin_ctz(cand0) + 1; s.lv0 = depth; s.nw0 = true; }
-        if (n1) { s.v1 = __builtin_ctz(cand1) + 1; s.lv1 = depth; s.nw1 = true; }
+        s.v0 = n0 ? __builtin_ctz(cand0) + 1 : s.v0;
+        s.lv0 = n0 ? depth : s.lv0;
+        s.v1 = n1 ? __builtin_ctz(cand1) + 1 : s.v1;
+        s.lv1 = n1 ? depth : s.lv1;
+        s.nw0 = n0;
+        s.nw1 = n1;
         placed = true;
         return PROP_OPEN;
     }
@@ -220,8 +229,10 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     // ---- phase B: hidden singles and digits with no place in a unit.
     // Cells publish their candidates; lanes 0..26 each gather one unit's nine
     // cells (conflict-light plain reads) and fold "seen once / seen twice".
+    // A unit whose givens clash publishes T = all digits, which switches the
+    // hidden-single rule off there without any test on the cell side.
     W.C[lane] = cand0;
-    if (s.has1) W.C[64 + lane] = cand1;
+    W.C[64 + lane] = cand1;  // lanes >= 17 land in padding
     wave_lds_sync();
     bool udead = false;
     if (lane < 27) {
@@ -232,26 +243,22 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
             twice |= once & x;
             once |= x;
         }
-        W.T[lane] = twice;
-        if (!((bad >> lane) & 1u)) udead = (once | W.M[lane]) != 0x1FFu;
+        const bool ok = !((bad >> lane) & 1u);
+        W.T[lane] = ok ? twice : 0x1FFu;
+        udead = ok && (once | W.M[lane]) != 0x1FFu;
     }
     wave_lds_sync();
-    uint32_t h0 = 0, h1 = 0;
-    if (e0) {
-        if (!((bad >> s.r0) & 1u)) h0 |= cand0 & ~W.T[s.r0];
-        if (!((bad >> (9 + s.c0)) & 1u)) h0 |= cand0 & ~W.T[9 + s.c0];
-        if (!((bad >> (18 + s.b0)) & 1u)) h0 |= cand0 & ~W.T[18 + s.b0];
-    }
-    if (e1) {
-        if (!((bad >> s.r1) & 1u)) h1 |= cand1 & ~W.T[s.r1];
-        if (!((bad >> (9 + s.c1)) & 1u)) h1 |= cand1 & ~W.T[9 + s.c1];
-        if (!((bad >> (18 + s.b1)) & 1u)) h1 |= cand1 & ~W.T[18 + s.b1];
-    }
+    const uint32_t h0 = cand0 & ~(W.T[s.r0] & W.T[9 + s.c0] & W.T[18 + s.b0]);
+    const uint32_t h1 = cand1 & ~(W.T[s.r1] & W.T[9 + s.c1] & W.T[18 + s.b1]);
     const bool dead2 = udead || (h0 & (h0 - 1)) != 0 || (h1 & (h1 - 1)) != 0;
     if (__any(dead2)) return PROP_DEAD;
     if (__any(h0 != 0 || h1 != 0)) {
-        if (h0) { s.v0 = __builtin_ctz(h0) + 1; s.lv0 = depth; s.nw0 = true; }
-        if (h1) { s.v1 = __builtin_ctz(h1) + 1; s.lv1 = depth; s.nw1 = true; }
+        s.v0 = h0 ? __builtin_ctz(h0) + 1 : s.v0;
+        s.lv0 = h0 ? depth : s.lv0;
+        s.v1 = h1 ? __builtin_ctz(h1) + 1 : s.v1;
+        s.lv1 = h1 ? depth : s.lv1;
+        s.nw0 = h0 != 0;
+        s.nw1 = h1 != 0;
         placed = true;
     }
     return PROP_OPEN;
@@ -431,6 +438,491 @@ __global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
         atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
         atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
         atomicAdd(&ws[WS_SWEEPS], (unsigned long long)sweeps);
+    }
+}
+
+// ====================================================== v3: two boards / wave
+// Half h = lane >> 5 of the wavefront owns one board; lane q = lane & 31 owns
+// cells q, 32+q and (q < 17) 64+q, and lanes q < 27 are that board's unit
+// lanes (row / column / box q) for the hidden-single gather.  Every VALU,
+// SALU and LDS instruction -- and every LDS round trip -- then serves two
+// boards, and 81 of the 96 cell slots are live (v2: 81 of 128).  Each half
+// keeps its own LDS slice, trail, stack (three VGPRs, level k at lane
+// 32h + (k & 31) of register k >> 5) and board cursor; per-half decisions
+// come from the two 32-bit halves of each ballot.  Same walk, same
+// propagation rules as v2, so the same first completion.
+
+struct __attribute__((aligned(16))) HalfLds {
+    uint32_t M[28];  // unit masks of filled cells
+    uint32_t T[28];  // per unit: digits that are candidates of >= 2 empty cells
+    uint32_t C[96];  // per cell slot: candidates published for the gather
+    uint32_t bad;    // units whose givens clash
+    uint32_t pad[3];
+};
+
+enum { H_STUCK = 0, H_DEAD = 1, H_SOLVED = 2, H_PLACED = 3, H_NEEDB = 4, H_IDLE = 5 };
+
+struct Lane3 {
+    uint32_t v[3], lv[3];
+    uint32_t gbits;   // bit s: slot s holds a given
+    uint32_t nwbits;  // bit s: slot s placed since the last sweep
+    int ur[3], uc[3], ub[3];
+    int ga[9];        // unit lanes: cells gathered for unit q
+    int q, h;
+    bool has2;        // slot 2 exists (q < 17)
+};
+
+struct HalfState {
+    uint32_t p, end;  // current board, end of the current chunk (n < 2^32 - chunk, checked on the host)
+    int act;          // a board is loaded
+    int rebuild;
+    uint32_t depth, bad;
+    uint32_t nguess;  // guesses on the current board (cancellation polling)
+};
+
+__device__ __forceinline__ void init_lane3(Lane3 &s, int lane)
+{
+    s.h = lane >> 5;
+    s.q = lane & 31;
+    s.has2 = s.q < 17;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int cell = (k < 2 || s.has2) ? 32 * k + s.q : 80;
+        int r, c, b;
+        cell_units(cell, r, c, b);
+        s.ur[k] = r;
+        s.uc[k] = 9 + c;
+        s.ub[k] = 18 + b;
+    }
+    const int u = s.q < 27 ? s.q : 0;
+    int base, s1, s2;
+    if (u < 9) { base = 9 * u; s1 = 1; s2 = 0; }
+    else if (u < 18) { base = u - 9; s1 = 9; s2 = 0; }
+    else { const int b = u - 18; base = (b / 3) * 27 + (b % 3) * 3; s1 = 1; s2 = 6; }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) s.ga[k] = base + k * s1 + (k / 3) * s2;
+    s.gbits = 0;
+    s.nwbits = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) { s.v[k] = 0; s.lv[k] = 0; }
+}
+
+__device__ __forceinline__ bool slot_ok(const Lane3 &s, int k) { return k < 2 || s.has2; }
+
+// Load board `p` into half X.  Returns false if a byte is > 9 (then the
+// half's cells hold the raw bytes for the write-back).
+template <int X>
+__device__ __forceinline__ bool load_half(const uint8_t *__restrict__ src, Lane3 &s)
+{
+    bool bad = false;
+    if (s.h == X) {
+        s.gbits = 0;
+        s.nwbits = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const uint32_t x = slot_ok(s, k) ? (uint32_t)src[32 * k + s.q] : 0u;
+            s.v[k] = x;
+            s.lv[k] = 0;
+            if (x) s.gbits |= 1u << k;
+            bad |= x > 9;
+        }
+    }
+    const uint64_t b = __ballot(bad);
+    return (X == 0 ? (uint32_t)b : (uint32_t)(b >> 32)) == 0;
+}
+
+// Givens' unit masks of half X into L.M (and the lanes' gmask), clash mask.
+template <int X>
+__device__ __forceinline__ uint32_t build_half_masks(HalfLds &L, const Lane3 &s, uint32_t &gmask)
+{
+    if (s.h == X) {
+        if (s.q < 28) L.M[s.q] = 0;
+        if (s.q == 0) L.bad = 0;
+    }
+    wave_lds_sync();
+    if (s.h == X) {
+        uint32_t d = 0;
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if ((s.gbits >> k) & 1u) {
+                const uint32_t bit = 1u << (s.v[k] - 1);
+                if (atomicOr(&L.M[s.ur[k]], bit) & bit) d |= 1u << s.ur[k];
+                if (atomicOr(&L.M[s.uc[k]], bit) & bit) d |= 1u << s.uc[k];
+                if (atomicOr(&L.M[s.ub[k]], bit) & bit) d |= 1u << s.ub[k];
+            }
+        }
+        if (d) atomicOr(&L.bad, d);
+    }
+    wave_lds_sync();
+    if (s.h == X && s.q < 27) gmask = L.M[s.q];
+    return (uint32_t)__builtin_amdgcn_readlane((int)L.bad, 32 * X);
+}
+
+__device__ __forceinline__ int half_status(uint32_t dead, uint32_t empty, uint32_t naked, int act)
+{
+    return !act ? H_IDLE : dead ? H_DEAD : !empty ? H_SOLVED : naked ? H_PLACED : H_NEEDB;
+}
+
+// One sweep of both halves.  lane-level inputs: gmask, the lane's half's
+// bad units, depth and rebuild flag; outputs per-half statuses.
+__device__ __forceinline__ void sweep3(HalfLds &L, Lane3 &s, uint32_t gmask, int act0, int act1, int rb0, int rb1,
+                                       uint32_t bad0, uint32_t bad1, uint32_t depth0, uint32_t depth1,
+                                       uint32_t (&cand)[3], int &st0, int &st1)
+{
+    // per-lane views of the two halves' uniform state (values, never a
+    // pointer select: that would push the state to scratch)
+    const bool mine0 = s.h == 0;
+    const bool act = mine0 ? act0 != 0 : act1 != 0;
+    const bool rb = mine0 ? rb0 != 0 : rb1 != 0;
+    const uint32_t bad = mine0 ? bad0 : bad1;
+    const uint32_t depth = mine0 ? depth0 : depth1;
+    const bool any_rb = rb0 || rb1;
+
+    // ---- phase A: unit masks up to date, clash detection
+    if (any_rb && rb && s.q < 27) L.M[s.q] = gmask;
+    uint32_t f = 0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool filled_nongiven = slot_ok(s, k) && s.v[k] != 0 && !((s.gbits >> k) & 1u);
+        const bool fk = act && (rb ? filled_nongiven : ((s.nwbits >> k) & 1u));
+        f |= (uint32_t)fk << k;
+    }
+    s.nwbits = 0;
+    uint32_t clash = 0;
+    if (any_rb || __any(f != 0)) {
+        wave_lds_sync();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if ((f >> k) & 1u) {
+                const uint32_t bit = 1u << (s.v[k] - 1);
+                clash |= (atomicOr(&L.M[s.ur[k]], bit) | atomicOr(&L.M[s.uc[k]], bit) |
+                          atomicOr(&L.M[s.ub[k]], bit)) & bit;
+            }
+        }
+    }
+    wave_lds_sync();
+    bool dead = clash != 0, anyempty = false, naked = false;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const bool e = act && slot_ok(s, k) && s.v[k] == 0;
+        cand[k] = e ? (~(L.M[s.ur[k]] | L.M[s.uc[k]] | L.M[s.ub[k]]) & 0x1FFu) : 0u;
+        dead |= e && cand[k] == 0;
+        anyempty |= e;
+        naked |= e && (cand[k] & (cand[k] - 1)) == 0;
+    }
+    const uint64_t bd = __ballot(dead), be = __ballot(anyempty), bn = __ballot(naked);
+    st0 = half_status((uint32_t)bd, (uint32_t)be, (uint32_t)bn, act0);
+    st1 = half_status((uint32_t)(bd >> 32), (uint32_t)(be >> 32), (uint32_t)(bn >> 32), act1);
+    const int mst = mine0 ? st0 : st1;
+    if (mst == H_PLACED) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (cand[k] != 0 && (cand[k] & (cand[k] - 1)) == 0) {
+                s.v[k] = __builtin_ctz(cand[k]) + 1;
+                s.lv[k] = depth;
+                s.nwbits |= 1u << k;
+            }
+        }
+    }
+    if (st0 != H_NEEDB && st1 != H_NEEDB) return;
+
+    // ---- phase B: hidden singles (halves in H_NEEDB only)
+    const bool needb = mst == H_NEEDB;
+#pragma unroll
+    for (int k = 0; k < 3; ++k)
+        if (slot_ok(s, k)) L.C[32 * k + s.q] = cand[k];
+    wave_lds_sync();
+    bool udead = false;
+    if (needb && s.q < 27) {
+        uint32_t once = 0, twice = 0;
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const uint32_t x = L.C[s.ga[k]];
+            twice |= once & x;
+            once |= x;
+        }
+        L.T[s.q] = twice;
+        if (!((bad >> s.q) & 1u)) udead = (once | L.M[s.q]) != 0x1FFu;
+    }
+    wave_lds_sync();
+    bool dead2 = udead, hid = false;
+    uint32_t hm[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        uint32_t x = 0;
+        if (needb && cand[k] != 0) {
+            if (!((bad >> s.ur[k]) & 1u)) x |= cand[k] & ~L.T[s.ur[k]];
+            if (!((bad >> s.uc[k]) & 1u)) x |= cand[k] & ~L.T[s.uc[k]];
+            if (!((bad >> s.ub[k]) & 1u)) x |= cand[k] & ~L.T[s.ub[k]];
+        }
+        hm[k] = x;
+        dead2 |= (x & (x - 1)) != 0;
+        hid |= x != 0;
+    }
+    const uint64_t bd2 = __ballot(dead2), bh = __ballot(hid);
+    if (st0 == H_NEEDB) st0 = (uint32_t)bd2 ? H_DEAD : (uint32_t)bh ? H_PLACED : H_STUCK;
+    if (st1 == H_NEEDB) st1 = (uint32_t)(bd2 >> 32) ? H_DEAD : (uint32_t)(bh >> 32) ? H_PLACED : H_STUCK;
+    if (needb && (mine0 ? st0 : st1) == H_PLACED) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (hm[k]) {
+                s.v[k] = __builtin_ctz(hm[k]) + 1;
+                s.lv[k] = depth;
+                s.nwbits |= 1u << k;
+            }
+        }
+    }
+}
+
+template <int X>
+__device__ __forceinline__ uint32_t rd_half(uint32_t v, int q) { return rdlane(v, 32 * X + q); }
+
+// place digit bit d at `cell` of half X with fill level `level`
+template <int X>
+__device__ __forceinline__ void place3(Lane3 &s, int cell, uint32_t dbit, uint32_t level)
+{
+    const bool hit = s.h == X && s.q == (cell & 31);
+    const int k = cell >> 5;
+    const uint32_t v = __builtin_ctz(dbit) + 1;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {  // static slot index: keeps the cells in VGPRs
+        if (hit && k == j) {
+            s.v[j] = v;
+            s.lv[j] = level;
+            s.nwbits |= 1u << j;
+        }
+    }
+}
+
+// Three named VGPRs, never an array: a select between array elements turns
+// into a dynamic index and pushes the array to scratch.
+struct Reg3 {
+    uint32_t a, b, c;
+};
+
+template <int X>
+__device__ __forceinline__ void stk_write(Reg3 &stk, const Lane3 &s, uint32_t level, uint32_t val)
+{
+    const bool me = s.h == X && s.q == (int)(level & 31);
+    if (level < 32) { if (me) stk.a = val; }
+    else if (level < 64) { if (me) stk.b = val; }
+    else { if (me) stk.c = val; }
+}
+
+template <int X>
+__device__ __forceinline__ uint32_t reg3_read(const Reg3 &r, uint32_t idx)
+{
+    if (idx < 32) return rd_half<X>(r.a, (int)idx);
+    if (idx < 64) return rd_half<X>(r.b, (int)(idx - 32));
+    return rd_half<X>(r.c, (int)(idx - 64));
+}
+
+template <int X>
+__device__ __forceinline__ uint32_t stk_read(const Reg3 &stk, uint32_t level) { return reg3_read<X>(stk, level); }
+
+// Branch half X on the walk's next cell (state is a fixpoint).
+template <int X>
+__device__ __forceinline__ bool guess3(Lane3 &s, Reg3 &stk, HalfState &H, const Reg3 &cand, int order)
+{
+    const bool me = s.h == X;
+    const uint64_t e0 = __ballot(me && s.v[0] == 0), e1 = __ballot(me && s.v[1] == 0),
+                   e2 = __ballot(me && s.has2 && s.v[2] == 0);
+    const uint32_t E0 = X ? (uint32_t)(e0 >> 32) : (uint32_t)e0;
+    const uint32_t E1 = X ? (uint32_t)(e1 >> 32) : (uint32_t)e1;
+    const uint32_t E2 = X ? (uint32_t)(e2 >> 32) : (uint32_t)e2;
+    const int cell = order_cell((uint64_t)E0 | ((uint64_t)E1 << 32), (uint64_t)E2, order);
+    const uint32_t c = reg3_read<X>(cand, (uint32_t)cell);
+    if (c == 0) return false;  // unreachable at a fixpoint
+    const uint32_t d = lowbit(c);
+    stk_write<X>(stk, s, H.depth, ((uint32_t)cell << 9) | (c ^ d));
+    H.depth++;
+    place3<X>(s, cell, d, H.depth);
+    H.nguess++;
+    return true;
+}
+
+// Backtrack half X; returns false when the tree is exhausted (unsolvable).
+template <int X>
+__device__ __forceinline__ bool backtrack3(Lane3 &s, Reg3 &stk, HalfState &H)
+{
+    H.rebuild = 1;
+    if (s.h == X) s.nwbits = 0;
+    for (;;) {
+        if (H.depth == 0) return false;
+        const uint32_t top = H.depth - 1;
+        const uint32_t entry = stk_read<X>(stk, top);
+        if (s.h == X) {
+#pragma unroll
+            for (int k = 0; k < 3; ++k)
+                if (s.lv[k] >= H.depth) s.v[k] = 0;
+        }
+        H.depth = top;
+        const uint32_t rem = entry & 0x1FFu;
+        if (rem == 0) continue;
+        const int cell = (int)(entry >> 9);
+        const uint32_t d = lowbit(rem);
+        stk_write<X>(stk, s, H.depth, ((uint32_t)cell << 9) | (rem ^ d));
+        H.depth++;
+        place3<X>(s, cell, d, H.depth);
+        H.nguess++;
+        return true;
+    }
+}
+
+template <int X>
+__device__ __forceinline__ void store_half(uint8_t *__restrict__ dst, const Lane3 &s, bool original)
+{
+    if (s.h == X) {
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            if (!slot_ok(s, k)) continue;
+            const uint32_t x = original ? (((s.gbits >> k) & 1u) ? s.v[k] : 0u) : s.v[k];
+            dst[32 * k + s.q] = (uint8_t)x;
+        }
+    }
+}
+
+struct Solve3Ctx {
+    const uint8_t *puzzles;
+    uint8_t *sols;
+    int32_t *status;
+    int64_t n, chunk, static_end;
+    unsigned long long *ws;
+    const int64_t *best;
+    int order;
+    uint32_t fin, solved, guesses, sweeps;
+};
+
+// Advance half X to its next board (chunk cursor, then the global queue) and
+// load it; sets H.act = 0 when the queue is drained.
+template <int X>
+__device__ __forceinline__ void next_board(HalfLds &L, Lane3 &s, HalfState &H, uint32_t &gmask, Solve3Ctx &c)
+{
+    int act = 0;
+    for (;;) {
+        H.p++;
+        if (H.p >= H.end) {
+            uint32_t t = 0;
+            if (s.h == X && s.q == 0) t = atomicAdd((unsigned int *)&c.ws[WS_QUEUE], 1u);
+            const uint64_t base = c.static_end + (uint64_t)rd_half<X>(t, 0) * c.chunk;
+            const uint64_t end = base + c.chunk < c.n ? base + c.chunk : c.n;
+            H.p = base < c.n ? (uint32_t)base : (uint32_t)c.n;
+            H.end = (uint32_t)end;
+        }
+        if (H.p >= c.n) break;
+        const uint8_t *src = c.puzzles + (uint64_t)H.p * 81;
+        uint8_t *dst = c.sols + (uint64_t)H.p * 81;
+        if (!load_half<X>(src, s)) {  // byte > 9: raw input back
+            store_half<X>(dst, s, false);
+            if (s.h == X && s.q == 0) c.status[H.p] = SDK_INVALID;
+            c.fin++;
+            continue;
+        }
+        if (c.best && __hip_atomic_load(c.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int64_t)H.p) {
+            store_half<X>(dst, s, true);
+            if (s.h == X && s.q == 0) c.status[H.p] = SDK_CANCELLED;
+            c.fin++;
+            continue;
+        }
+        H.bad = build_half_masks<X>(L, s, gmask);
+        act = 1;
+        break;
+    }
+    // one assignment point per field: stores of equal constants to different
+    // fields on two paths get merged behind a pointer phi, which pins the
+    // state to scratch
+    H.act = act;
+    H.rebuild = 0;
+    H.depth = 0;
+    H.nguess = 0;
+}
+
+template <int X>
+__device__ __forceinline__ void finish_board(HalfLds &L, Lane3 &s, HalfState &H, uint32_t &gmask, Solve3Ctx &c,
+                                             int st)
+{
+    uint8_t *dst = c.sols + (uint64_t)H.p * 81;
+    store_half<X>(dst, s, st != SDK_SOLVED);
+    if (s.h == X && s.q == 0) c.status[H.p] = st;
+    if (st == SDK_SOLVED) {
+        c.solved++;
+        if (c.best && s.h == X && s.q == 0)
+            __hip_atomic_fetch_min((int64_t *)&c.ws[WS_BEST], (int64_t)H.p, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+    c.fin++;
+    c.guesses += H.nguess;
+    next_board<X>(L, s, H, gmask, c);
+}
+
+template <int X>
+__device__ __forceinline__ void step_half(HalfLds &L, Lane3 &s, Reg3 &stk, HalfState &H, uint32_t &gmask,
+                                          const Reg3 &cand, Solve3Ctx &c, int st)
+{
+    if (st == H_SOLVED) {
+        finish_board<X>(L, s, H, gmask, c, SDK_SOLVED);
+    } else if (st == H_DEAD) {
+        if (!backtrack3<X>(s, stk, H)) finish_board<X>(L, s, H, gmask, c, SDK_UNSOLVABLE);
+    } else if (st == H_STUCK) {
+        if (!guess3<X>(s, stk, H, cand, c.order)) {
+            finish_board<X>(L, s, H, gmask, c, SDK_FAULT);
+        } else if (c.best && (H.nguess & 63u) == 0 &&
+                   __hip_atomic_load(c.best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (int64_t)H.p) {
+            finish_board<X>(L, s, H, gmask, c, SDK_CANCELLED);
+        }
+    }
+}
+
+__global__ __launch_bounds__(BLOCK_THREADS) void solve2_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered, int order)
+{
+    __shared__ HalfLds lds[WAVES_PER_BLOCK][2];
+    const int lane = threadIdx.x & 63;
+    Lane3 s;
+    init_lane3(s, lane);
+    HalfLds &L = lds[threadIdx.x >> 6][s.h];
+    const int64_t slots = (int64_t)gridDim.x * WAVES_PER_BLOCK * 2;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+
+    Solve3Ctx c;
+    c.puzzles = puzzles; c.sols = sols; c.status = status; c.n = n; c.chunk = chunk;
+    c.static_end = slots * chunk; c.ws = ws; c.order = order;
+    c.best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+    c.fin = c.solved = c.guesses = c.sweeps = 0;
+
+    HalfState H0, H1;
+    uint32_t gmask = 0;
+    Reg3 stk = {0u, 0u, 0u};
+    // static first chunk of each half (the cursor starts one before it)
+    {
+        const int64_t b0 = (2 * gw) * chunk, b1 = (2 * gw + 1) * chunk;
+        H0.p = (uint32_t)(b0 < n ? b0 : n) - 1u;  // the cursor starts one before its chunk
+        H1.p = (uint32_t)(b1 < n ? b1 : n) - 1u;
+        H0.end = (uint32_t)(b0 + chunk < n ? b0 + chunk : n);
+        H1.end = (uint32_t)(b1 + chunk < n ? b1 + chunk : n);
+    }
+    H0.act = H1.act = 0;
+    next_board<0>(L, s, H0, gmask, c);
+    next_board<1>(L, s, H1, gmask, c);
+
+    uint32_t cand[3];
+    while (H0.act || H1.act) {
+        int st0, st1;
+        sweep3(L, s, gmask, H0.act, H1.act, H0.rebuild, H1.rebuild, H0.bad, H1.bad, H0.depth, H1.depth, cand,
+               st0, st1);
+        const Reg3 cr = {cand[0], cand[1], cand[2]};
+        c.sweeps += (uint32_t)H0.act + (uint32_t)H1.act;
+        H0.rebuild = 0;
+        H1.rebuild = 0;
+        step_half<0>(L, s, stk, H0, gmask, cr, c, st0);
+        step_half<1>(L, s, stk, H1, gmask, cr, c, st1);
+    }
+    if (lane == 0 && c.fin) {
+        atomicAdd(&ws[WS_FINISHED], (unsigned long long)c.fin);
+        atomicAdd(&ws[WS_SOLVED], (unsigned long long)c.solved);
+        atomicAdd(&ws[WS_GUESSES], (unsigned long long)c.guesses);
+        atomicAdd(&ws[WS_SWEEPS], (unsigned long long)c.sweeps);
     }
 }
 
@@ -646,23 +1138,42 @@ static int cu_count()
     return g_cu_count[dev];
 }
 
-static int solve_blocks_per_cu()
+template <typename K>
+static int blocks_per_cu(K kernel, std::atomic<int> &cached)
 {
-    static std::atomic<int> cached{0};
     int v = cached.load();
     if (v) return v;
     int nb = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, solve_kernel, BLOCK_THREADS, 0) != hipSuccess || nb <= 0)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, BLOCK_THREADS, 0) != hipSuccess || nb <= 0)
         nb = 4;
     if (nb > 8) nb = 8;
     cached.store(nb);
     return nb;
 }
+static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0};
+
+// kernel variant: 2 = one board per wave (default), 3 = two boards per wave
+// (SDK_SOLVE_KERNEL=3; measured slower on MI355X)
+static int solve_variant()
+{
+    static std::atomic<int> v{0};
+    int x = v.load();
+    if (!x) {
+        const char *e = getenv("SDK_SOLVE_KERNEL");
+        x = (e && e[0] == '3') ? 3 : 2;
+        v.store(x);
+    }
+    return x;
+}
 
 extern "C" {
 
 const char *sdk_last_error(void) { return g_err; }
-const char *sdk_version(void) { return "sudoku_hip 0.1 gfx950 wave-per-board walk-order"; }
+const char *sdk_version(void)
+{
+    return solve_variant() == 3 ? "sudoku_hip 0.2 gfx950 two-boards-per-wave walk-order"
+                                : "sudoku_hip 0.2 gfx950 wave-per-board walk-order";
+}
 int sdk_device_cu_count(void) { return cu_count(); }
 size_t sdk_workspace_bytes(void) { return WS_WORDS * sizeof(unsigned long long); }
 
@@ -679,15 +1190,30 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     unsigned long long *ws = (unsigned long long *)d_workspace;
     hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     hipError_t e;
-    // persistent grid: exactly the resident waves (occupancy query, cached)
-    const int64_t max_waves = (int64_t)cu_count() * solve_blocks_per_cu() * WAVES_PER_BLOCK;
-    int64_t waves = n < max_waves ? n : max_waves;
-    int64_t chunk = n / (waves * 16);
-    if (chunk < 1) chunk = 1;
-    if (chunk > 16) chunk = 16;
-    const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
-    hipLaunchKernelGGL(solve_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
-                       d_status, n, ws, chunk, ordered, order);
+    if (solve_variant() == 3) {
+        if (n > (int64_t)0xFFFF0000u) {
+            snprintf(g_err, sizeof g_err, "sdk_solve_batch: n=%lld exceeds 2^32-2^16 boards per call", (long long)n);
+            return -2;
+        }
+        // persistent grid of exactly the resident waves, two board slots each
+        const int64_t max_slots = (int64_t)cu_count() * blocks_per_cu(solve2_kernel, g_bpc_v3) * WAVES_PER_BLOCK * 2;
+        const int64_t slots = n < max_slots ? n : max_slots;
+        int64_t chunk = n / (slots * 16);
+        if (chunk < 1) chunk = 1;
+        if (chunk > 16) chunk = 16;
+        const int64_t blocks = (slots + 2 * WAVES_PER_BLOCK - 1) / (2 * WAVES_PER_BLOCK);
+        hipLaunchKernelGGL(solve2_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
+                           d_status, n, ws, chunk, ordered, order);
+    } else {
+        const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solve_kernel, g_bpc_v2) * WAVES_PER_BLOCK;
+        const int64_t waves = n < max_waves ? n : max_waves;
+        int64_t chunk = n / (waves * 16);
+        if (chunk < 1) chunk = 1;
+        if (chunk > 16) chunk = 16;
+        const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+        hipLaunchKernelGGL(solve_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
+                           d_status, n, ws, chunk, ordered, order);
+    }
     e = hipGetLastError();
     if (e != hipSuccess) return set_err("sdk_solve_batch: launch", e);
     return 0;
