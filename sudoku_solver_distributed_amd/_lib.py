@@ -10,7 +10,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsudoku_hip.so")
+# SDK_LIB selects another in-tree build of the same ABI (A/B experiments)
+LIB_PATH = os.environ.get("SDK_LIB") or os.path.join(_HERE, "libsudoku_hip.so")
 
 SDK_UNSOLVABLE = 0
 SDK_SOLVED = 1
