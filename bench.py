@@ -45,6 +45,49 @@ def cpu_baseline(boards, budget_s: float):
     return done, time.perf_counter() - t0
 
 
+def _time(fn, reps=3):
+    import torch
+    best = None
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        out = fn()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+    return best, out
+
+
+def side_configs(solver, dev, world, rank):
+    """BASELINE.json configs[1] and configs[3], outside the timed region.
+
+    configs[1]: 100k gen.py-style boards (generate_sudoku(50) under one seed,
+    same random calls as gen.py:31-52) solved in one batch on one GPU.
+    configs[3]: one search-heavy board, the walk's direct single-wave solve
+    vs the frontier split (over every rank's GPU when N > 1, RCCL
+    all-reduce(MIN) early-exit word).  Every result is checked.
+    """
+    import torch
+    from sudoku_solver_distributed_amd.distributed import solve_split
+    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, generate_batch
+    out = {}
+    if rank == 0:
+        gen = generate_batch(100_000, 50, seed=7, device=dev)
+        t, (sols, st) = _time(lambda: solver.solve(gen))
+        ok = bool((st == 1).all()) and bool((solver.check(sols, 0) == 1).all())
+        out["gen100k"] = {"boards": 100_000, "empty_boxes": 50, "seconds": t, "boards_per_s": 100_000 / t,
+                          "all_solved_and_checked": ok}
+    board = torch.tensor([[int(c) for c in SEARCH_HEAVY]], dtype=torch.uint8, device=dev)
+    t_direct, (g1, s1) = _time(lambda: solver.solve(board))
+    st = {}
+    t_split, (ok2, g2) = _time(lambda: solve_split(board, order="gen", target=4096, stats=st))
+    same = bool(int(s1[0]) == 1 and ok2 and torch.equal(g1[0].cpu(), g2.cpu()))
+    out["pathological"] = {"board": SEARCH_HEAVY, "direct_ms": t_direct * 1e3, "split_ms": t_split * 1e3,
+                           "ranks": world, "frontier": st.get("frontier"), "rounds": st.get("rounds"),
+                           "identical": same}
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -56,6 +99,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-boards", type=int, default=32,
                     help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the configs[1] / configs[3] side measurements")
     args = ap.parse_args()
 
     import torch
@@ -122,6 +167,8 @@ def main():
     lat.sort()
     p50 = lat[len(lat) // 2] if lat else None
 
+    extras = None if args.no_extras else side_configs(solver, dev, world, rank)
+
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -176,6 +223,7 @@ def main():
         "sweeps_per_board": st["sweeps"] / max(st["finished"], 1),
         "roofline": roof,
         "cpu_baseline": cpu,
+        "side_configs": extras,
     }
     print(json.dumps(line), flush=True)
     if world > 1:
