@@ -89,6 +89,16 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
  * (INT64_MAX if none), out[5] reserved.  reset != 0 zeroes them afterwards. */
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 
+/* Solve-kernel selection (library extension, no reference counterpart):
+ * SDK_KERNEL_WAVE (default) one wavefront per board; SDK_KERNEL_PAIR two
+ * boards per wavefront; SDK_KERNEL_LANE one lane per board.  All give the
+ * same results.  0 restores the default (or $SDK_SOLVE_KERNEL = 2|3|l).
+ * Returns the previous selection, -1 for an unknown value. */
+#define SDK_KERNEL_WAVE 2
+#define SDK_KERNEL_PAIR 3
+#define SDK_KERNEL_LANE 4
+int sdk_set_solve_kernel(int kernel);
+
 /* Library / device info. */
 const char *sdk_last_error(void);
 const char *sdk_version(void);

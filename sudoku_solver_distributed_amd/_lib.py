@@ -32,7 +32,9 @@ EXPORTS = (
     "sdk_last_error",
     "sdk_version",
     "sdk_device_cu_count",
+    "sdk_set_solve_kernel",
 )
+SDK_KERNELS = {"wave": 2, "pair": 3, "lane": 4}
 
 _lib = None
 
@@ -70,6 +72,8 @@ def load() -> ctypes.CDLL:
     L.sdk_version.argtypes = []
     L.sdk_device_cu_count.restype = i32
     L.sdk_device_cu_count.argtypes = []
+    L.sdk_set_solve_kernel.restype = i32
+    L.sdk_set_solve_kernel.argtypes = [i32]
     _lib = L
     return L
 

@@ -23,7 +23,8 @@ def hipcc() -> str:
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
-    deps = [SRC, os.path.join(ROOT, "include", "sudoku_hip.h")]
+    csrc = os.path.join(_HERE, "csrc")
+    deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include", "sudoku_hip.h")]
     if (not force and os.path.exists(OUT)
             and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
         return OUT

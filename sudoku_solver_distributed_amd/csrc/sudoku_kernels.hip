@@ -40,6 +40,7 @@
 #include <stdlib.h>
 
 #include "../../include/sudoku_hip.h"
+#include "lane_solver.h"
 
 #define WAVES_PER_BLOCK 4
 #define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
@@ -926,6 +927,148 @@ __global__ __launch_bounds__(BLOCK_THREADS) void solve2_kernel(
     }
 }
 
+// ====================================================== lane-per-board kernel
+// Each LANE owns one board (lane_solver.h: unit masks in registers, fully
+// unrolled Gauss-Seidel passes, DFS stack in per-lane scratch).  The loop is
+// a per-lane state machine -- every iteration runs one naked pass, a hidden
+// pass for the lanes whose naked pass stalled, then each lane's own guess /
+// backtrack / finish -- and a lane that finishes pulls its next board from
+// the queue in the same iteration, so lanes of a wave never wait for a
+// slower board.
+
+struct ScratchStack {
+    uint32_t w[lane::MAX_DEPTH * lane::STACK_WORDS];
+    __device__ __forceinline__ void put(uint32_t d, int k, uint32_t v) { w[d * lane::STACK_WORDS + k] = v; }
+    __device__ __forceinline__ uint32_t get(uint32_t d, int k) const { return w[d * lane::STACK_WORDS + k]; }
+};
+
+__global__ __launch_bounds__(BLOCK_THREADS) void lane_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, int ordered, int order)
+{
+    ScratchStack stk;
+    lane::Board b;
+    const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+    int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // first board: static
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+    const int node_order = order == SDK_ORDER_NODE;
+    uint32_t depth = 0, nguess = 0;
+    uint32_t fin = 0, solved = 0, guesses = 0, passes = 0;
+    bool have = false;
+
+    for (;;) {
+        // ---- refill: lanes without a board take the next one
+        while (!have) {
+            if (p >= n) break;
+            const uint8_t *src = puzzles + p * 81;
+            const bool valid = lane::load_dw(b, src);
+            if (!valid) {
+                for (int i = 0; i < 81; ++i) sols[p * 81 + i] = src[i];
+                status[p] = SDK_INVALID;
+                fin++;
+            } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
+                for (int i = 0; i < 81; ++i) sols[p * 81 + i] = src[i];
+                status[p] = SDK_CANCELLED;
+                fin++;
+            } else {
+                depth = 0;
+                nguess = 0;
+                have = true;
+                break;
+            }
+            p = nthreads + (int64_t)atomicAdd(&ws[WS_QUEUE], 1ull);
+        }
+        if (!__any(have)) break;
+        if (!have) continue;
+
+        // ---- one propagation step
+        uint32_t dead = 0, placed = 0;
+        lane::NakedPass<0>::run(b, dead, placed);
+        passes++;
+        const bool empty = (b.E[0] | b.E[1] | b.E[2]) != 0;
+        if (!dead && !placed && empty) {
+            lane::HiddenPass<0>::run(b, dead, placed);
+            passes++;
+        }
+        int done = -1;  // board status when it finishes in this step
+        if (!dead) {
+            if (!(b.E[0] | b.E[1] | b.E[2])) {
+                done = SDK_SOLVED;
+            } else if (!placed) {
+                // branch on the walk's next cell, smallest digit first
+                const int cell = lane::order_cell((uint64_t)b.E[0] | ((uint64_t)b.E[1] << 32),
+                                                  (uint64_t)b.E[2], node_order);
+                const uint32_t cand = lane::cand_at(b, cell);
+                const uint32_t d = cand & (0u - cand);
+#pragma unroll
+                for (int w = 0; w < 11; ++w) stk.put(depth, w, b.V[w]);
+#pragma unroll
+                for (int w = 0; w < 3; ++w) stk.put(depth, 11 + w, b.E[w]);
+                stk.put(depth, lane::STACK_ENTRY, ((uint32_t)cell << 9) | (cand ^ d));
+                depth++;
+                nguess++;
+                lane::place_at(b, cell, d);
+                if (best && (nguess & 63u) == 0 &&
+                    __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)
+                    done = SDK_CANCELLED;
+            }
+        } else {
+            // back to the deepest level with an untried digit
+            done = SDK_UNSOLVABLE;
+            while (depth > 0) {
+                depth--;
+                const uint32_t entry = stk.get(depth, lane::STACK_ENTRY);
+                const uint32_t rem = entry & 0x1FFu;
+                if (!rem) continue;
+                const int cell = (int)(entry >> 9);
+                const uint32_t d = rem & (0u - rem);
+#pragma unroll
+                for (int w = 0; w < 11; ++w) b.V[w] = stk.get(depth, w);
+#pragma unroll
+                for (int w = 0; w < 3; ++w) b.E[w] = stk.get(depth, 11 + w);
+                lane::rebuild_units(b);
+                stk.put(depth, lane::STACK_ENTRY, ((uint32_t)cell << 9) | (rem ^ d));
+                depth++;
+                nguess++;
+                lane::place_at(b, cell, d);
+                done = -1;
+                break;
+            }
+        }
+        if (done >= -2 && done != -1) {
+            uint8_t *dst = sols + p * 81;
+            if (done == SDK_SOLVED) {
+                lane::store(b, dst);
+                solved++;
+                if (best)
+                    __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                const uint8_t *src = puzzles + p * 81;
+                for (int i = 0; i < 81; ++i) dst[i] = src[i];
+            }
+            status[p] = done;
+            fin++;
+            guesses += nguess;
+            have = false;
+            p = nthreads + (int64_t)atomicAdd(&ws[WS_QUEUE], 1ull);
+        }
+    }
+    // per-wave statistics
+    unsigned long long f = fin, sv = solved, g = guesses, ps = passes;
+    for (int o = 32; o > 0; o >>= 1) {
+        f += __shfl_xor(f, o);
+        sv += __shfl_xor(sv, o);
+        g += __shfl_xor(g, o);
+        ps += __shfl_xor(ps, o);
+    }
+    if ((threadIdx.x & 63) == 0 && f) {
+        atomicAdd(&ws[WS_FINISHED], f);
+        atomicAdd(&ws[WS_SOLVED], sv);
+        atomicAdd(&ws[WS_GUESSES], g);
+        atomicAdd(&ws[WS_SWEEPS], ps);
+    }
+}
+
 // ------------------------------------------------------------ check kernel
 // One thread per grid; the block stages its 64 grids (5184 B) through LDS
 // with coalesced dword loads.
@@ -1150,18 +1293,24 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
     cached.store(nb);
     return nb;
 }
-static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0};
+static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0};
 
 // kernel variant: 2 = one board per wave (default), 3 = two boards per wave
 // (SDK_SOLVE_KERNEL=3; measured slower on MI355X)
+static std::atomic<int> g_variant{0};
+
+static int env_variant()
+{
+    const char *e = getenv("SDK_SOLVE_KERNEL");
+    return (e && e[0] == '3') ? SDK_KERNEL_PAIR : (e && e[0] == 'l') ? SDK_KERNEL_LANE : SDK_KERNEL_WAVE;
+}
+
 static int solve_variant()
 {
-    static std::atomic<int> v{0};
-    int x = v.load();
+    int x = g_variant.load();
     if (!x) {
-        const char *e = getenv("SDK_SOLVE_KERNEL");
-        x = (e && e[0] == '3') ? 3 : 2;
-        v.store(x);
+        x = env_variant();
+        g_variant.store(x);
     }
     return x;
 }
@@ -1171,10 +1320,20 @@ extern "C" {
 const char *sdk_last_error(void) { return g_err; }
 const char *sdk_version(void)
 {
-    return solve_variant() == 3 ? "sudoku_hip 0.2 gfx950 two-boards-per-wave walk-order"
-                                : "sudoku_hip 0.2 gfx950 wave-per-board walk-order";
+    const int v = solve_variant();
+    return v == SDK_KERNEL_LANE ? "sudoku_hip 0.3 gfx950 lane-per-board walk-order"
+         : v == SDK_KERNEL_PAIR ? "sudoku_hip 0.3 gfx950 board-pair-per-wave walk-order"
+                  : "sudoku_hip 0.3 gfx950 wave-per-board walk-order";
 }
 int sdk_device_cu_count(void) { return cu_count(); }
+int sdk_set_solve_kernel(int kernel)
+{
+    if (kernel != 0 && kernel != SDK_KERNEL_WAVE && kernel != SDK_KERNEL_PAIR && kernel != SDK_KERNEL_LANE)
+        return -1;
+    const int prev = solve_variant();
+    g_variant.store(kernel ? kernel : env_variant());
+    return prev;
+}
 size_t sdk_workspace_bytes(void) { return WS_WORDS * sizeof(unsigned long long); }
 
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
@@ -1190,7 +1349,15 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     unsigned long long *ws = (unsigned long long *)d_workspace;
     hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     hipError_t e;
-    if (solve_variant() == 3) {
+    const int variant = solve_variant();
+    if (variant == SDK_KERNEL_LANE) {
+        // lane per board: one persistent thread per resident lane
+        const int64_t max_threads = (int64_t)cu_count() * blocks_per_cu(lane_kernel, g_bpc_lane) * BLOCK_THREADS;
+        const int64_t threads = n < max_threads ? n : max_threads;
+        const int64_t blocks = (threads + BLOCK_THREADS - 1) / BLOCK_THREADS;
+        hipLaunchKernelGGL(lane_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
+                           d_status, n, ws, ordered, order);
+    } else if (variant == SDK_KERNEL_PAIR) {
         if (n > (int64_t)0xFFFF0000u) {
             snprintf(g_err, sizeof g_err, "sdk_solve_batch: n=%lld exceeds 2^32-2^16 boards per call", (long long)n);
             return -2;

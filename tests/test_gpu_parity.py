@@ -252,3 +252,47 @@ def test_distributed_single_rank_gpu(solver):
     assert (lo, hi) == (0, 1000) and bool((sts == 1).all())
     w, c = O.solve_unique_batch(b.numpy())
     assert np.array_equal(sols.cpu().numpy(), w)
+
+
+@pytest.mark.parametrize("kernel", ["pair", "lane"])
+def test_alternate_kernels_parity(solver, kernel):
+    """The non-default solve kernels (sdk_set_solve_kernel): goldens, generated
+    boards in both walks, clashing givens, invalid bytes, ordered mode and
+    hard 17-clue boards -- bit-identical to the oracle like the default."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch
+    prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
+    assert prev > 0
+    try:
+        assert kernel.encode() in solver.lib.sdk_version()
+        cases = load_golden("golden_gen.json")
+        sols, st = solver.solve(torch.tensor([b81(c["puzzle"]) for c in cases], dtype=torch.uint8))
+        for c, o, s in zip(cases, sols.cpu().numpy(), st.cpu().numpy()):
+            assert (s == 1) == c["solved"] and _s(o) == c["solution"], c["seed"]
+        for order in ("gen", "node"):
+            full = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
+            dup = "88" + full[2:30] + "0" + full[31:50] + "0" + full[51:70] + "0" + full[71:]
+            edge = np.array([b81(x) for x in (full, "5" * 81, dup, "0" * 81)], dtype=np.uint8)
+            puzzles = np.concatenate([generate_batch(96, 55, seed=4321).cpu().numpy(), edge])
+            sols, st = solver.solve(torch.from_numpy(puzzles), order=order)
+            want, wst = O.solve_batch(puzzles, order=order)
+            assert np.array_equal(st.cpu().numpy(), wst), order
+            assert np.array_equal(sols.cpu().numpy(), want), order
+        raw = torch.zeros((3, 81), dtype=torch.uint8, device=solver.device)
+        raw[1, 80] = 10
+        raw[2, 0] = 255
+        sols, st = solver.solve(raw)
+        assert st.cpu().tolist() == [1, -1, -1] and int(sols[1, 80]) == 10
+        p = hard17_batch(2000, seed=5)
+        sols, st = solver.solve(p)
+        want, cnt = O.solve_unique_batch(p.numpy())
+        assert (st.cpu().numpy() == 1).all() and np.array_equal(sols.cpu().numpy(), want)
+        p = hard17_batch(64, seed=11)
+        p[:10, :] = torch.tensor(b81("123456780000000009" + "0" * 63), dtype=torch.uint8)
+        solver.stats(reset=True)
+        sols, st = solver.solve(p, ordered=True)
+        st = st.cpu().numpy()
+        assert (st[:10] == 0).all() and st[10] == 1 and set(np.unique(st[11:])) <= {1, -2}
+        assert solver.stats()["best"] == 10
+    finally:
+        solver.lib.sdk_set_solve_kernel(prev)
