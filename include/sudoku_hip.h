@@ -97,6 +97,7 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 #define SDK_KERNEL_WAVE 2
 #define SDK_KERNEL_PAIR 3
 #define SDK_KERNEL_LANE 4
+#define SDK_KERNEL_PACKED 5
 int sdk_set_solve_kernel(int kernel);
 
 /* Library / device info. */

@@ -34,7 +34,7 @@ EXPORTS = (
     "sdk_device_cu_count",
     "sdk_set_solve_kernel",
 )
-SDK_KERNELS = {"wave": 2, "pair": 3, "lane": 4}
+SDK_KERNELS = {"wave": 2, "pair": 3, "lane": 4, "packed": 5}
 
 _lib = None
 

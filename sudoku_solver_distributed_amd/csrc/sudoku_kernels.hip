@@ -77,6 +77,27 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_wave_barrier();
 }
 
+// Order this wave's LDS accesses for the compiler only.  A wavefront's DS
+// instructions execute in issue order, so a lane's read issued after another
+// lane's write/atomic of the same word sees it without waiting for the
+// write's return: the sweep's round trips (atomics -> mask reads, publish ->
+// gather -> T reads) overlap in the LDS pipeline instead of each draining
+// lgkmcnt.  The signal fence keeps the compiler from moving accesses across.
+#ifndef SDK_LDS_INORDER
+#define SDK_LDS_INORDER 0
+#endif
+__device__ __forceinline__ void wave_lds_order()
+{
+#if SDK_LDS_INORDER
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    wave_lds_sync();
+#endif
+}
+
+// wave-uniform "any lane": the ballot's SGPR pair, no VGPR round trip
+__device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
 __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
 {
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
@@ -126,7 +147,7 @@ __device__ __forceinline__ bool load_board(const uint8_t *__restrict__ src, int 
     s.lv1 = 0;
     s.nw0 = false;
     s.nw1 = false;
-    return !__any(a > 9 || b > 9);
+    return !wany(a > 9 || b > 9);
 }
 
 // Build the givens' unit masks (returned in lanes 0..26; W.M holds them on
@@ -135,7 +156,7 @@ __device__ __forceinline__ uint32_t build_given_masks(WaveLds &W, int lane, cons
 {
     if (lane < 28) W.M[lane] = 0;
     if (lane == 0) W.bad = 0;
-    wave_lds_sync();
+    wave_lds_order();
     if (s.g0) {
         uint32_t bit = 1u << (s.v0 - 1);
         uint32_t d = 0;
@@ -152,7 +173,7 @@ __device__ __forceinline__ uint32_t build_given_masks(WaveLds &W, int lane, cons
         if (atomicOr(&W.M[18 + s.b1], bit) & bit) d |= 1u << (18 + s.b1);
         if (d) atomicOr(&W.bad, d);
     }
-    wave_lds_sync();
+    wave_lds_order();
     bad = __builtin_amdgcn_readfirstlane(W.bad);
     return lane < 27 ? W.M[lane] : 0u;
 }
@@ -186,8 +207,8 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     s.nw0 = false;
     s.nw1 = false;
     uint32_t clash = 0;
-    if (rebuild || __any(f0 || f1)) {
-        wave_lds_sync();
+    if (rebuild || wany(f0 || f1)) {
+        wave_lds_order();
         if (f0) {
             uint32_t bit = 1u << (s.v0 - 1);
             clash |= (atomicOr(&W.M[s.r0], bit) | atomicOr(&W.M[9 + s.c0], bit) |
@@ -198,7 +219,7 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
             clash |= (atomicOr(&W.M[s.r1], bit) | atomicOr(&W.M[9 + s.c1], bit) |
                       atomicOr(&W.M[18 + s.b1], bit)) & bit;
         }
-        wave_lds_sync();
+        wave_lds_order();
     }
     rebuild = false;
     const bool e0 = s.v0 == 0;
@@ -210,13 +231,13 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     cand0 = e0 ? (~m0 & 0x1FFu) : 0u;
     cand1 = e1 ? (~m1 & 0x1FFu) : 0u;
     const bool dead = clash != 0 || (e0 && cand0 == 0) || (e1 && cand1 == 0);
-    if (__any(dead)) return PROP_DEAD;
-    if (!__any(e0 || e1)) return PROP_SOLVED;
+    if (wany(dead)) return PROP_DEAD;
+    if (!wany(e0 || e1)) return PROP_SOLVED;
 
     // ---- naked singles
     const bool n0 = e0 && (cand0 & (cand0 - 1)) == 0;
     const bool n1 = e1 && (cand1 & (cand1 - 1)) == 0;
-    if (__any(n0 || n1)) {
+    if (wany(n0 || n1)) {
         s.v0 = n0 ? __builtin_ctz(cand0) + 1 : s.v0;
         s.lv0 = n0 ? depth : s.lv0;
         s.v1 = n1 ? __builtin_ctz(cand1) + 1 : s.v1;
@@ -234,7 +255,7 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
     // hidden-single rule off there without any test on the cell side.
     W.C[lane] = cand0;
     W.C[64 + lane] = cand1;  // lanes >= 17 land in padding
-    wave_lds_sync();
+    wave_lds_order();
     bool udead = false;
     if (lane < 27) {
         uint32_t once = 0, twice = 0;
@@ -248,12 +269,12 @@ __device__ __forceinline__ int sweep(WaveLds &W, int lane, Cells &s, uint32_t gm
         W.T[lane] = ok ? twice : 0x1FFu;
         udead = ok && (once | W.M[lane]) != 0x1FFu;
     }
-    wave_lds_sync();
+    wave_lds_order();
     const uint32_t h0 = cand0 & ~(W.T[s.r0] & W.T[9 + s.c0] & W.T[18 + s.b0]);
     const uint32_t h1 = cand1 & ~(W.T[s.r1] & W.T[9 + s.c1] & W.T[18 + s.b1]);
     const bool dead2 = udead || (h0 & (h0 - 1)) != 0 || (h1 & (h1 - 1)) != 0;
-    if (__any(dead2)) return PROP_DEAD;
-    if (__any(h0 != 0 || h1 != 0)) {
+    if (wany(dead2)) return PROP_DEAD;
+    if (wany(h0 != 0 || h1 != 0)) {
         s.v0 = h0 ? __builtin_ctz(h0) + 1 : s.v0;
         s.lv0 = h0 ? depth : s.lv0;
         s.v1 = h1 ? __builtin_ctz(h1) + 1 : s.v1;
@@ -386,7 +407,10 @@ __global__ void arm_kernel(unsigned long long *ws)
     if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
 }
 
-__global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
+#ifndef SDK_SOLVE_WAVES_PER_EU
+#define SDK_SOLVE_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(BLOCK_THREADS, SDK_SOLVE_WAVES_PER_EU) void solve_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
     int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered, int order)
 {
@@ -441,6 +465,9 @@ __global__ __launch_bounds__(BLOCK_THREADS) void solve_kernel(
         atomicAdd(&ws[WS_SWEEPS], (unsigned long long)sweeps);
     }
 }
+
+// ====================================================== v4: packed cell pairs
+#include "packed_solver.h"
 
 // ====================================================== v3: two boards / wave
 // Half h = lane >> 5 of the wavefront owns one board; lane q = lane & 31 owns
@@ -1293,7 +1320,7 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
     cached.store(nb);
     return nb;
 }
-static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0};
+static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0}, g_bpc_v4{0};
 
 // kernel variant: 2 = one board per wave (default), 3 = two boards per wave
 // (SDK_SOLVE_KERNEL=3; measured slower on MI355X)
@@ -1302,7 +1329,8 @@ static std::atomic<int> g_variant{0};
 static int env_variant()
 {
     const char *e = getenv("SDK_SOLVE_KERNEL");
-    return (e && e[0] == '3') ? SDK_KERNEL_PAIR : (e && e[0] == 'l') ? SDK_KERNEL_LANE : SDK_KERNEL_WAVE;
+    return (e && e[0] == '3') ? SDK_KERNEL_PAIR : (e && e[0] == 'l') ? SDK_KERNEL_LANE
+         : (e && e[0] == 'p') ? SDK_KERNEL_PACKED : SDK_KERNEL_WAVE;
 }
 
 static int solve_variant()
@@ -1322,13 +1350,15 @@ const char *sdk_version(void)
 {
     const int v = solve_variant();
     return v == SDK_KERNEL_LANE ? "sudoku_hip 0.3 gfx950 lane-per-board walk-order"
+         : v == SDK_KERNEL_PACKED ? "sudoku_hip 0.4 gfx950 wave-per-board packed-pairs walk-order"
          : v == SDK_KERNEL_PAIR ? "sudoku_hip 0.3 gfx950 board-pair-per-wave walk-order"
                   : "sudoku_hip 0.3 gfx950 wave-per-board walk-order";
 }
 int sdk_device_cu_count(void) { return cu_count(); }
 int sdk_set_solve_kernel(int kernel)
 {
-    if (kernel != 0 && kernel != SDK_KERNEL_WAVE && kernel != SDK_KERNEL_PAIR && kernel != SDK_KERNEL_LANE)
+    if (kernel != 0 && kernel != SDK_KERNEL_WAVE && kernel != SDK_KERNEL_PAIR && kernel != SDK_KERNEL_LANE &&
+        kernel != SDK_KERNEL_PACKED)
         return -1;
     const int prev = solve_variant();
     g_variant.store(kernel ? kernel : env_variant());
@@ -1370,6 +1400,15 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
         if (chunk > 16) chunk = 16;
         const int64_t blocks = (slots + 2 * WAVES_PER_BLOCK - 1) / (2 * WAVES_PER_BLOCK);
         hipLaunchKernelGGL(solve2_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
+                           d_status, n, ws, chunk, ordered, order);
+    } else if (variant == SDK_KERNEL_PACKED) {
+        const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_kernel, g_bpc_v4) * WAVES_PER_BLOCK;
+        const int64_t waves = n < max_waves ? n : max_waves;
+        int64_t chunk = n / (waves * 16);
+        if (chunk < 1) chunk = 1;
+        if (chunk > 16) chunk = 16;
+        const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
+        hipLaunchKernelGGL(solvep_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
                            d_status, n, ws, chunk, ordered, order);
     } else {
         const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solve_kernel, g_bpc_v2) * WAVES_PER_BLOCK;
