@@ -34,7 +34,7 @@ sys.path.insert(0, ROOT)
 PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 PEAK_HBM = 8.0e12                       # B/s (MI355X_MICROARCH.md)
 BYTES_PER_BOARD = 81 + 81 + 4           # board in, board out, status
-PMC_FILE = os.path.join(ROOT, "profiles", "pmc_solve_kernel.json")
+PMC_DIR = os.path.join(ROOT, "profiles")   # pmc_<kernel symbol>.json (scripts/gpu_pmc.sh)
 
 
 def cpu_baseline(boards, budget_s: float):
@@ -182,10 +182,14 @@ def main():
             "hbm": {"achieved_GBps": BYTES_PER_BOARD * args.batch / kern_s / 1e9,
                     "peak_GBps": PEAK_HBM / 1e9,
                     "frac": BYTES_PER_BOARD * args.batch / kern_s / PEAK_HBM}}
+    from sudoku_solver_distributed_amd import _lib
+    kname = _lib.KERNEL_SYMBOLS.get(_lib.active_kernel(), "?")
+    roof["kernel"] = kname
+    PMC_FILE = os.path.join(PMC_DIR, f"pmc_{kname}.json")
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("batch") == args.batch and pmc.get("seed") == args.seed:
+        if pmc.get("batch") == args.batch and pmc.get("seed") == args.seed and pmc.get("kernel") == kname:
             ops = pmc["valu_insts_per_launch"] * 64
             roof["achieved"] = ops / kern_s / 1e12
             roof["frac"] = roof["achieved"] / roof["peak"]

@@ -90,9 +90,11 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 
 /* Solve-kernel selection (library extension, no reference counterpart):
- * SDK_KERNEL_WAVE (default) one wavefront per board; SDK_KERNEL_PAIR two
- * boards per wavefront; SDK_KERNEL_LANE one lane per board.  All give the
- * same results.  0 restores the default (or $SDK_SOLVE_KERNEL = 2|3|l).
+ * SDK_KERNEL_PACKED (default) one wavefront per board, both cells of a lane
+ * packed in one word; SDK_KERNEL_WAVE one wavefront per board, one register
+ * set per cell; SDK_KERNEL_PAIR two boards per wavefront; SDK_KERNEL_LANE one
+ * lane per board.  All give the same results.  0 restores the default (or
+ * $SDK_SOLVE_KERNEL = p|2|3|l).
  * Returns the previous selection, -1 for an unknown value. */
 #define SDK_KERNEL_WAVE 2
 #define SDK_KERNEL_PAIR 3

@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${BATCH:-1048576}
-CMD="python -u bench.py --steps 2 --warmup 1 --batch $B --no-cpu --latency-boards 0"
+CMD="python -u bench.py --steps 2 --warmup 1 --batch $B --no-cpu --latency-boards 0 --no-extras"
 run() {  # name counters...
   local name=$1; shift
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- $CMD > gpurun_out/pmc_$name.log 2>&1
@@ -13,4 +13,5 @@ run valu SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUS
 run wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
-python scripts/pmc_summarize.py gpurun_out/pmc_solve_kernel.json $B 2024 gpurun_out/pmc_valu gpurun_out/pmc_wait gpurun_out/pmc_fetch gpurun_out/pmc_write
+K=${PMC_KERNEL:-solvep_kernel}
+PMC_KERNEL=$K python scripts/pmc_summarize.py gpurun_out/pmc_$K.json $B 2024 gpurun_out/pmc_valu gpurun_out/pmc_wait gpurun_out/pmc_fetch gpurun_out/pmc_write

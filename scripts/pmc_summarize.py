@@ -1,5 +1,5 @@
 """Summarise rocprofv3 --pmc passes for the solve kernel into
-profiles/pmc_solve_kernel.json (read by bench.py for the VALU roofline).
+profiles/pmc_<kernel>.json (read by bench.py for the VALU roofline).
 
     python scripts/pmc_summarize.py OUT.json BATCH SEED DIR [DIR ...]
 
@@ -30,7 +30,7 @@ def main():
     vals = defaultdict(list)
     for d in dirs:
         rows = [r for r in load(d) if r.get("Kernel_Name", "").split("(")[0] in
-                ((kernel,) if kernel else ("solve_kernel", "solve2_kernel"))]
+                ((kernel,) if kernel else ("solvep_kernel",))]
         if not rows:
             continue
         gmax = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
@@ -42,9 +42,7 @@ def main():
         for (disp, name), v in per.items():
             vals[name].append(v)
     summary = {k: sum(v) / len(v) for k, v in vals.items()}
-    names = sorted({r.get("Kernel_Name", "").split("(")[0] for d in dirs for r in load(d)
-                    if r.get("Kernel_Name", "").startswith("solve")})
-    res = {"kernel": ",".join(names), "batch": batch, "seed": seed,
+    res = {"kernel": kernel or "solvep_kernel", "batch": batch, "seed": seed,
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),
            "hbm_bytes_per_launch": None}

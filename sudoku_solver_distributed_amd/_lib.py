@@ -35,6 +35,8 @@ EXPORTS = (
     "sdk_set_solve_kernel",
 )
 SDK_KERNELS = {"wave": 2, "pair": 3, "lane": 4, "packed": 5}
+# device symbol of each solve kernel (rocprofv3 Kernel_Name, profiles/pmc_<symbol>.json)
+KERNEL_SYMBOLS = {2: "solve_kernel", 3: "solve2_kernel", 4: "lane_kernel", 5: "solvep_kernel"}
 
 _lib = None
 
@@ -76,6 +78,14 @@ def load() -> ctypes.CDLL:
     L.sdk_set_solve_kernel.argtypes = [i32]
     _lib = L
     return L
+
+
+def active_kernel() -> int:
+    """The solve kernel sdk_solve_batch launches now (SDK_KERNEL_*)."""
+    L = load()
+    cur = L.sdk_set_solve_kernel(0)
+    L.sdk_set_solve_kernel(cur)
+    return cur
 
 
 def check(rc: int, what: str) -> None:

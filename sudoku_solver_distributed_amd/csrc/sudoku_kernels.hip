@@ -1322,15 +1322,17 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
 }
 static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0}, g_bpc_v4{0};
 
-// kernel variant: 2 = one board per wave (default), 3 = two boards per wave
-// (SDK_SOLVE_KERNEL=3; measured slower on MI355X)
+// kernel variant: 5 = one board per wave, packed cell pairs (default);
+// 2 = one board per wave, one register set per cell slot (SDK_SOLVE_KERNEL=2);
+// 3 = two boards per wave (=3), 4 = one board per lane (=l): measured slower
+// on MI355X, see DESIGN.md
 static std::atomic<int> g_variant{0};
 
 static int env_variant()
 {
     const char *e = getenv("SDK_SOLVE_KERNEL");
     return (e && e[0] == '3') ? SDK_KERNEL_PAIR : (e && e[0] == 'l') ? SDK_KERNEL_LANE
-         : (e && e[0] == 'p') ? SDK_KERNEL_PACKED : SDK_KERNEL_WAVE;
+         : (e && (e[0] == '2' || e[0] == 'w')) ? SDK_KERNEL_WAVE : SDK_KERNEL_PACKED;
 }
 
 static int solve_variant()
