@@ -225,6 +225,7 @@ def main():
         "all_solved_and_checked": solved_ok,
         "guesses_per_board": st["guesses"] / max(st["finished"], 1),
         "sweeps_per_board": st["sweeps"] / max(st["finished"], 1),
+        "deferred_per_step": st.get("deferred", 0) / args.steps,
         "roofline": roof,
         "cpu_baseline": cpu,
         "side_configs": extras,

@@ -36,9 +36,10 @@ extern "C" {
                              has one (its scan breaks only the inner loop) */
 #define SDK_ORDER_NODE 1  /* node.py:62-74: first empty cell, row-major      */
 
-/* Bytes of device workspace sdk_solve_batch needs (queue heads, cancel word,
- * statistics).  Allocate once, zero once; the library re-arms the per-call
- * words itself with a hipMemsetAsync on `stream`. */
+/* Bytes of device workspace sdk_solve_batch needs on the current device:
+ * queue heads, cancel word, statistics, and the plane kernel's per-lane DFS
+ * stacks (about 1.5 GB on an MI355X).  Allocate once per device and stream,
+ * zero once; the library re-arms the per-call words itself on `stream`. */
 size_t sdk_workspace_bytes(void);
 
 /* Solve n boards.  For every board the output is the FIRST solution of the
@@ -86,20 +87,27 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
 /* Copy statistics to host (synchronous on `stream`):
  * out[0] boards finished, out[1] boards solved, out[2] guesses (DFS nodes),
  * out[3] propagation sweeps, out[4] lowest solved index in ordered mode
- * (INT64_MAX if none), out[5] reserved.  reset != 0 zeroes them afterwards. */
+ * (INT64_MAX if none), out[5] boards the plane kernel handed to the
+ * wave-per-board pass (clashing givens, searches deeper than its stack).  reset != 0 zeroes them afterwards. */
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 
 /* Solve-kernel selection (library extension, no reference counterpart):
- * SDK_KERNEL_PACKED (default) one wavefront per board, both cells of a lane
- * packed in one word; SDK_KERNEL_WAVE one wavefront per board, one register
+ * SDK_KERNEL_AUTO (default) SDK_KERNEL_PLANE for batches of 8192 boards or
+ * more, SDK_KERNEL_PACKED below; SDK_KERNEL_PLANE one lane per board on
+ * digit-plane bitboards
+ * (boards with clashing givens or very deep searches go to a second,
+ * wave-per-board pass); SDK_KERNEL_PACKED one wavefront per board, both cells
+ * of a lane packed in one word; SDK_KERNEL_WAVE one wavefront per board, one register
  * set per cell; SDK_KERNEL_PAIR two boards per wavefront; SDK_KERNEL_LANE one
- * lane per board.  All give the same results.  0 restores the default (or
- * $SDK_SOLVE_KERNEL = p|2|3|l).
+ * lane per board, nibble cells.  All give the same results.  0 restores the
+ * default (or $SDK_SOLVE_KERNEL = auto|plane|p|2|3|l).
  * Returns the previous selection, -1 for an unknown value. */
+#define SDK_KERNEL_AUTO 1
 #define SDK_KERNEL_WAVE 2
 #define SDK_KERNEL_PAIR 3
 #define SDK_KERNEL_LANE 4
 #define SDK_KERNEL_PACKED 5
+#define SDK_KERNEL_PLANE 6
 int sdk_set_solve_kernel(int kernel);
 
 /* Library / device info. */

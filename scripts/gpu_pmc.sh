@@ -13,5 +13,5 @@ run valu SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUS
 run wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_ACTIVE_INST_LDS SQ_INSTS_BRANCH GRBM_GUI_ACTIVE GRBM_COUNT || exit 1
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
-K=${PMC_KERNEL:-solvep_kernel}
+K=${PMC_KERNEL:-plane_kernel}
 PMC_KERNEL=$K python scripts/pmc_summarize.py gpurun_out/pmc_$K.json $B 2024 gpurun_out/pmc_valu gpurun_out/pmc_wait gpurun_out/pmc_fetch gpurun_out/pmc_write

@@ -30,7 +30,7 @@ def main():
     vals = defaultdict(list)
     for d in dirs:
         rows = [r for r in load(d) if r.get("Kernel_Name", "").split("(")[0] in
-                ((kernel,) if kernel else ("solvep_kernel",))]
+                ((kernel,) if kernel else ("plane_kernel",))]
         if not rows:
             continue
         gmax = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
@@ -42,7 +42,7 @@ def main():
         for (disp, name), v in per.items():
             vals[name].append(v)
     summary = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"kernel": kernel or "solvep_kernel", "batch": batch, "seed": seed,
+    res = {"kernel": kernel or "plane_kernel", "batch": batch, "seed": seed,
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),
            "hbm_bytes_per_launch": None}

@@ -10,7 +10,9 @@ import sys
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
-SRC = os.path.join(_HERE, "csrc", "sudoku_kernels.hip")
+# translation units and their extra flags (plane_kernels.hip: see its header)
+SRCS = (("sudoku_kernels.hip", []),
+        ("plane_kernels.hip", ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]))
 OUT = os.path.join(_HERE, "libsudoku_hip.so")
 ARCH = os.environ.get("SDK_OFFLOAD_ARCH", "gfx950")
 
@@ -22,20 +24,36 @@ def hipcc() -> str:
     return "hipcc"
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT) -> str:
+    """Compile every translation unit for gfx950 and link the C-ABI library.
+    `defines` / `out`: A/B builds of tuning macros into another in-tree .so
+    (loaded with SDK_LIB=...)."""
     csrc = os.path.join(_HERE, "csrc")
-    deps = [os.path.join(csrc, f) for f in os.listdir(csrc)] + [os.path.join(ROOT, "include", "sudoku_hip.h")]
-    if (not force and os.path.exists(OUT)
-            and all(os.path.getmtime(OUT) >= os.path.getmtime(d) for d in deps)):
-        return OUT
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-shared", "-fPIC",
-           "-Wall", "-o", OUT + ".tmp", SRC]
-    if verbose:
-        cmd.append("-Rpass-analysis=kernel-resource-usage")
-    subprocess.check_call(cmd)
-    os.replace(OUT + ".tmp", OUT)
-    return OUT
+    deps = [os.path.join(csrc, f) for f in os.listdir(csrc) if not f.endswith(".o")] + [os.path.join(ROOT, "include", "sudoku_hip.h")]
+    if (not force and os.path.exists(out)
+            and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)):
+        return out
+    objs = []
+    for name, extra in SRCS:
+        obj = out + "." + name + ".o"
+        cmd = [hipcc(), f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall", *extra,
+               *[f"-D{d}" for d in defines],
+               "-c", "-o", obj, os.path.join(csrc, name)]
+        if verbose:
+            cmd.append("-Rpass-analysis=kernel-resource-usage")
+        subprocess.check_call(cmd)
+        objs.append(obj)
+    subprocess.check_call([hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out + ".tmp", *objs])
+    for obj in objs:
+        os.remove(obj)
+    os.replace(out + ".tmp", out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose="-v" in sys.argv))
+    # python -m sudoku_solver_distributed_amd.build [--force] [-v] [--tag T -DNAME=V ...]
+    args = sys.argv[1:]
+    defs = [a[2:] for a in args if a.startswith("-D")]
+    tag = args[args.index("--tag") + 1] if "--tag" in args else None
+    dst = os.path.join(_HERE, f"libsudoku_hip_{tag}.so") if tag else OUT
+    print(build(force="--force" in args or bool(tag), verbose="-v" in args, defines=defs, out=dst))

@@ -1,0 +1,87 @@
+// common.h -- definitions shared by the solve kernels' translation units
+// (sudoku_kernels.hip: wave-per-board kernels + C ABI; plane_kernels.hip: the
+// lane-per-board digit-plane kernel, built with its own scheduler options).
+#ifndef SDK_COMMON_H
+#define SDK_COMMON_H
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/sudoku_hip.h"
+
+#define WAVES_PER_BLOCK 4
+// internal status of a board the plane kernel leaves to the packed kernel
+// (never visible to callers: the deferred pass overwrites it)
+#define SDK_DEFERRED 0x7FFF0001
+#define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
+
+// ---------------------------------------------------------------- workspace
+// word layout of the device workspace (uint64 words)
+enum {
+    WS_QUEUE = 0,      // chunked board queue head (re-armed every call)
+    WS_BEST = 1,       // ordered mode: lowest solved index (re-armed to INT64_MAX)
+    WS_ARM_WORDS = 2,  // words re-armed per call
+    WS_STACK_BYTE = 256,  // the plane kernel's per-lane stacks start here
+    WS_FINISHED = 8,   // statistics (accumulate until sdk_read_stats(reset))
+    WS_SOLVED = 9,
+    WS_GUESSES = 10,
+    WS_SWEEPS = 11,
+    WS_DEFERRED = 12,  // boards the plane kernel left to the packed kernel
+    WS_WORDS = 16
+};
+
+struct __attribute__((aligned(16))) WaveLds {
+    uint32_t M[28];  // unit masks of filled cells (rows 0-8, columns 9-17, boxes 18-26)
+    uint32_t T[28];  // per unit: digits that are candidates of >= 2 of its empty cells
+    uint32_t C[128]; // per cell: candidate mask published for the unit gather (0 = filled; 81.. padding)
+    uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
+    uint32_t pad[3];
+};
+
+__device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
+
+// Orders this wave's LDS accesses (a single wave's DS ops execute in order;
+// this keeps the compiler from moving them and drains returns).
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+    __builtin_amdgcn_wave_barrier();
+}
+
+// Order this wave's LDS accesses for the compiler only.  A wavefront's DS
+// instructions execute in issue order, so a lane's read issued after another
+// lane's write/atomic of the same word sees it without waiting for the
+// write's return: the sweep's round trips (atomics -> mask reads, publish ->
+// gather -> T reads) overlap in the LDS pipeline instead of each draining
+// lgkmcnt.  The signal fence keeps the compiler from moving accesses across.
+#ifndef SDK_LDS_INORDER
+#define SDK_LDS_INORDER 0
+#endif
+__device__ __forceinline__ void wave_lds_order()
+{
+#if SDK_LDS_INORDER
+    __atomic_signal_fence(__ATOMIC_SEQ_CST);
+#else
+    wave_lds_sync();
+#endif
+}
+
+// wave-uniform "any lane": the ballot's SGPR pair, no VGPR round trip
+__device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
+
+__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+
+// Launch the plane kernel (plane_kernels.hip) and report its occupancy.
+hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
+                            unsigned long long *ws, uint32_t *stack, int ordered, int order, int64_t threads,
+                            hipStream_t st);
+int sdk_plane_blocks_per_cu();
+#define PLANE_MAX_DEPTH 32
+#define PLANE_THREADS 256
+#define PLANE_STACK_WORDS 28
+
+#endif  // SDK_COMMON_H

@@ -312,6 +312,47 @@ __device__ __forceinline__ int psearch(PackLds &W, int lane, PCells &s, int64_t 
     }
 }
 
+// One board (index p) by the whole wave: load, search, store, status.
+__device__ __forceinline__ void psolve_board(PackLds &W, int lane, PCells &s, const uint8_t *__restrict__ puzzles,
+                                             uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t p,
+                                             unsigned long long *__restrict__ ws, const int64_t *best, int order,
+                                             uint32_t &solved, uint32_t &guesses, uint32_t &sweeps)
+{
+    const uint8_t *src = puzzles + p * 81;
+    uint8_t *dst = sols + p * 81;
+    uint32_t a, b;
+    int st;
+    if (!pload_board(src, lane, s, a, b)) {
+        st = SDK_INVALID;
+        dst[lane] = (uint8_t)a;  // raw input back
+        if (lane < 17) dst[64 + lane] = (uint8_t)b;
+    } else if (best && __builtin_amdgcn_readfirstlane((int)(
+                   __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p))) {
+        st = SDK_CANCELLED;
+        pstore_board(dst, lane, s, true);
+    } else {
+        st = psearch(W, lane, s, p, order, best, guesses, sweeps);
+        pstore_board(dst, lane, s, st != SDK_SOLVED);
+        if (st == SDK_SOLVED) {
+            solved++;
+            if (best && lane == 0)
+                __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    if (lane == 0) status[p] = st;
+}
+
+__device__ __forceinline__ void pflush_stats(int lane, unsigned long long *__restrict__ ws, uint32_t fin,
+                                             uint32_t solved, uint32_t guesses, uint32_t sweeps)
+{
+    if (lane == 0 && fin) {
+        atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
+        atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
+        atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
+        atomicAdd(&ws[WS_SWEEPS], (unsigned long long)sweeps);
+    }
+}
+
 #ifndef SDK_PACKED_WAVES_PER_EU
 #define SDK_PACKED_WAVES_PER_EU 1
 #endif
@@ -335,29 +376,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
     while (base < n) {
         const int64_t end = base + chunk < n ? base + chunk : n;
         for (int64_t p = base; p < end; ++p) {
-            const uint8_t *src = puzzles + p * 81;
-            uint8_t *dst = sols + p * 81;
-            uint32_t a, b;
-            int st;
-            if (!pload_board(src, lane, s, a, b)) {
-                st = SDK_INVALID;
-                dst[lane] = (uint8_t)a;  // raw input back
-                if (lane < 17) dst[64 + lane] = (uint8_t)b;
-            } else if (best && __builtin_amdgcn_readfirstlane((int)(
-                           __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p))) {
-                st = SDK_CANCELLED;
-                pstore_board(dst, lane, s, true);
-            } else {
-                st = psearch(W, lane, s, p, order, best, guesses, sweeps);
-                pstore_board(dst, lane, s, st != SDK_SOLVED);
-                if (st == SDK_SOLVED) {
-                    solved++;
-                    if (best && lane == 0)
-                        __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED,
-                                               __HIP_MEMORY_SCOPE_AGENT);
-                }
-            }
-            if (lane == 0) status[p] = st;
+            psolve_board(W, lane, s, puzzles, sols, status, p, ws, best, order, solved, guesses, sweeps);
             fin++;
         }
         unsigned long long t = 0;
@@ -365,12 +384,37 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
         t = __shfl(t, 0);
         base = static_end + (int64_t)t * chunk;
     }
-    if (lane == 0 && fin) {
-        atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
-        atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
-        atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
-        atomicAdd(&ws[WS_SWEEPS], (unsigned long long)sweeps);
+    pflush_stats(lane, ws, fin, solved, guesses, sweeps);
+}
+
+// Second pass behind the plane kernel: solve exactly the boards it left
+// (status SDK_DEFERRED).  Each wave scans 64 statuses per load and runs the
+// deferred ones among them, grid-stride over the batch.
+__global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep_deferred_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, int ordered, int order)
+{
+    __shared__ PackLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    PackLds &W = lds[threadIdx.x >> 6];
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+
+    PCells s;
+    pinit_lane(s, lane);
+    uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
+    for (int64_t base = gw * 64; base < n; base += nwaves * 64) {
+        const int32_t sv = base + lane < n ? status[base + lane] : 0;
+        uint64_t m = __builtin_amdgcn_ballot_w64(sv == SDK_DEFERRED);
+        while (m) {
+            const int j = __builtin_ctzll(m);
+            m &= m - 1;
+            psolve_board(W, lane, s, puzzles, sols, status, base + j, ws, best, order, solved, guesses, sweeps);
+            fin++;
+        }
     }
+    pflush_stats(lane, ws, fin, solved, guesses, sweeps);
 }
 
 #endif  // SDK_PACKED_SOLVER_H

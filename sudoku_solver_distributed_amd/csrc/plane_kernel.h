@@ -1,0 +1,280 @@
+// plane_kernel.h -- v5 solve kernel: one board per LANE on digit planes
+// (plane_solver.h), included by sudoku_kernels.hip after the packed kernel.
+//
+// Why a lane per board: the wave-per-board kernels spend ~1650 wave
+// instructions per hard board (29 sweeps x ~57), most of them masks for 81
+// cells spread over 64 lanes, LDS round trips and wave-uniform control.  On
+// digit planes one lane runs a whole pass over its board in ~1800 lane
+// instructions, i.e. ~28 wave instructions per board-pass, and a pass does
+// naked AND hidden singles for all cells (19 passes per hard board instead
+// of 29 sweeps).
+//
+// Execution: persistent lanes.  Each lane holds one board (27 plane words +
+// 3 bookkeeping words in VGPRs) and steps it one pass per loop iteration;
+// guesses push the 27 words to a per-lane stack in the caller's workspace
+// ([level][word][lane]: one level's words of the 64 lanes of a wave are
+// contiguous).  Finished lanes wait until at least SDK_PLANE_REFILL lanes of
+// the wave are free, then stores and refills run once for all of them: the
+// 81-byte load and store code is lane-divergent, so running it every
+// iteration for one lane would cost the whole wave.  Boards come from one
+// atomic queue head per wave refill.
+//
+// Boards the planes cannot take -- givens that repeat a digit in a unit
+// (rules B/C are unsound there, plane_solver.h) or a search deeper than
+// PLANE_MAX_DEPTH -- get status SDK_DEFERRED and no output; the packed
+// kernel then runs over the batch with deferred_only set and solves exactly
+// those.  Results are identical either way.
+#ifndef SDK_PLANE_KERNEL_H
+#define SDK_PLANE_KERNEL_H
+
+#include "plane_solver.h"
+
+#ifndef SDK_PLANE_REFILL
+#define SDK_PLANE_REFILL 8
+#endif
+static_assert(PLANE_STACK_WORDS == plane::STACK_WORDS, "stack layout");
+
+// Per-lane stack in the workspace: word w of level L of lane g lives at
+// dword (L*28 + w)*nt + g.  Buffer stores/loads: the lane part of the offset
+// is one VGPR (voffset), the word part is wave-uniform (soffset), so the 28
+// word addresses never become 28 hoisted 64-bit VGPR pairs.
+struct PlaneStack {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t lane_off;  // g * 4
+    uint32_t nt4;       // nt * 4: bytes per (level, word) row
+    __device__ __forceinline__ uint32_t voff(uint32_t level) const
+    {
+        return lane_off + level * (uint32_t)plane::STACK_WORDS * nt4;
+    }
+    __device__ __forceinline__ void put(uint32_t level, int w, uint32_t v) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, (int)voff(level), (int)((uint32_t)w * nt4), 0);
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t level, int w) const
+    {
+        return __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff(level), (int)((uint32_t)w * nt4), 0);
+    }
+};
+
+// Cooperative board I/O.  Loads and stores run for one board at a time over
+// the whole wave, in the band-word layout: lane l's slot 0 is bit (l & 31)
+// of band l >> 5 and its slot 1 bit l of band 2, so one ballot per digit and
+// slot yields that digit's band words directly (bits 9, 19, 29 and 30-31 of
+// a band word are no cell: those slots hold none).
+__device__ __forceinline__ int plane_slot_cell(int lane, int slot)
+{
+    const int band = slot ? 2 : (lane >> 5), pos = lane & 31;
+    if ((slot && lane >= 32) || pos >= 30 || pos % 10 == 9) return -1;
+    return 27 * band + 9 * (pos / 10) + pos % 10;
+}
+
+// copy board q's 81 bytes from src to dst (lanes l and 64 + l)
+__device__ __forceinline__ void plane_copy_board(const uint8_t *__restrict__ src, uint8_t *__restrict__ dst, int lane)
+{
+    dst[lane] = src[lane];
+    if (lane < 17) dst[64 + lane] = src[64 + lane];
+}
+
+// lane states; the two "original" states store the input board back
+enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
+
+// number of lanes executing this point (the exec mask of a divergent branch)
+__device__ __forceinline__ uint32_t lanes_here() { return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)); }
+
+#ifndef SDK_PLANE_WAVES_PER_EU
+#define SDK_PLANE_WAVES_PER_EU 2
+#endif
+__global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
+    unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int ordered, int order)
+{
+    const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
+    const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
+    const PlaneStack stk = {
+        __builtin_amdgcn_make_buffer_rsrc(stack, 0, (int)(nt * 4 * plane::STACK_WORDS * PLANE_MAX_DEPTH), 0x00020000),
+        (uint32_t)g * 4u, (uint32_t)nt * 4u};
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+    const int node_order = order == SDK_ORDER_NODE;
+    const int lane = threadIdx.x & 63;
+
+    plane::Board B;
+    int64_t p = -1;       // this lane's board
+    int state = PL_IDLE;
+    uint32_t depth = 0;
+    // wave-uniform statistics
+    uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
+    bool drained = false;  // the queue is empty
+
+    for (;;) {
+        const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
+        if (__builtin_popcountll(~active) >= SDK_PLANE_REFILL || active == 0) {
+            const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
+            // ---- store finished boards, one at a time over the whole wave
+            uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
+            solved += (uint32_t)__builtin_popcountll(m);
+            while (m) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                uint8_t *dst = sols + pi * 81;
+                const uint32_t pos = lane & 31;
+                uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    // value bit-slices of lane i's (solved) band b, wave-uniform
+                    uint32_t q[9];
+#pragma unroll
+                    for (int d = 0; d < 9; ++d) q[d] = rdlane(B.P[d][b], i);
+                    const uint32_t V[4] = {q[0] | q[2] | q[4] | q[6] | q[8],  // digits 1 3 5 7 9
+                                           q[1] | q[2] | q[5] | q[6],         // 2 3 6 7
+                                           q[3] | q[4] | q[5] | q[6],         // 4 5 6 7
+                                           q[7] | q[8]};                      // 8 9
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v |= ((V[k] >> pos) & 1u) << k;
+                    if (b == 0) v0 = lane < 32 ? v : v0;
+                    if (b == 1) v0 = lane >= 32 ? v : v0;
+                    if (b == 2) v1 = v;
+                }
+                if (c0 >= 0) dst[c0] = (uint8_t)v0;
+                if (c1 >= 0) dst[c1] = (uint8_t)v1;
+                if (lane == 0) status[pi] = SDK_SOLVED;
+            }
+            // ---- unsolvable / cancelled: the input board back
+            m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
+            while (m) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                plane_copy_board(puzzles + pi * 81, sols + pi * 81, lane);
+                if (lane == 0) status[pi] = rdlane((uint32_t)state, i) == PL_CANCELLED ? SDK_CANCELLED : SDK_UNSOLVABLE;
+            }
+            if (state != PL_ACTIVE) state = PL_IDLE;
+            // ---- refill the free lanes: one queue add per wave, then one
+            // board at a time over the whole wave
+            if (!drained) {
+                const uint64_t idle = ~active;
+                const int k = __builtin_popcountll(idle);
+                unsigned long long base = 0;
+                const int leader = __builtin_ctzll(idle);
+                if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)k);
+                base = __shfl(base, leader);
+                drained = (int64_t)base + k >= n;
+                uint32_t given[3] = {0u, 0u, 0u};
+                bool loaded = false;
+                m = idle;
+                for (int64_t q = (int64_t)base; m && q < n; ++q) {
+                    const int i = __builtin_ctzll(m);
+                    m &= m - 1;
+                    fin++;
+                    const uint8_t *src = puzzles + q * 81;
+                    const uint32_t a0 = c0 >= 0 ? src[c0] : 0xFFu, a1 = c1 >= 0 ? src[c1] : 0xFFu;
+                    if (__builtin_amdgcn_ballot_w64((a0 > 9 && a0 != 0xFFu) || (a1 > 9 && a1 != 0xFFu))) {
+                        plane_copy_board(src, sols + q * 81, lane);  // raw input back
+                        if (lane == 0) status[q] = SDK_INVALID;
+                        continue;
+                    }
+                    if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q) {
+                        plane_copy_board(src, sols + q * 81, lane);
+                        if (lane == 0) status[q] = SDK_CANCELLED;
+                        continue;
+                    }
+                    const uint64_t e0 = __builtin_amdgcn_ballot_w64(a0 == 0u);
+                    const uint32_t E[3] = {(uint32_t)e0, (uint32_t)(e0 >> 32),
+                                           (uint32_t)__builtin_amdgcn_ballot_w64(a1 == 0u)};
+#pragma unroll
+                    for (int d = 0; d < 9; ++d) {
+                        const uint64_t m0 = __builtin_amdgcn_ballot_w64(a0 == (uint32_t)(d + 1));
+                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_ballot_w64(a1 == (uint32_t)(d + 1));
+                        B.P[d][0] = lane == i ? ((uint32_t)m0 | E[0]) : B.P[d][0];
+                        B.P[d][1] = lane == i ? ((uint32_t)(m0 >> 32) | E[1]) : B.P[d][1];
+                        B.P[d][2] = lane == i ? (m1 | E[2]) : B.P[d][2];
+                    }
+                    if (lane == i) {
+#pragma unroll
+                        for (int b = 0; b < 3; ++b) given[b] = plane::ROWS & ~E[b];
+                        B.Det[0] = B.Det[1] = B.Det[2] = 0;
+                        p = q;
+                        depth = 0;
+                        loaded = true;
+                    }
+                }
+                // givens repeating a digit in a unit: the packed kernel's board
+                if (loaded) {
+                    if (plane::givens_clash(B, given)) {
+                        status[p] = SDK_DEFERRED;
+                        const uint32_t k = lanes_here();
+                        fin -= k;
+                        deferred += k;
+                    } else {
+                        state = PL_ACTIVE;
+                    }
+                }
+            }
+            if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;
+        }
+        if (state != PL_ACTIVE) continue;
+
+        // ---- one pass of this lane's board
+        passes += lanes_here();
+        uint32_t und[3];
+        const int r = plane::pass(B, und);
+        if (r == plane::SOLVED) {
+            state = PL_SOLVED;
+            if (best)
+                __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else if (r == plane::STUCK) {
+            if (depth == PLANE_MAX_DEPTH) {
+                status[p] = SDK_DEFERRED;  // too deep for the stack: the packed kernel's
+                const uint32_t k = lanes_here();
+                fin -= k;
+                deferred += k;
+                state = PL_IDLE;
+            } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
+                state = PL_CANCELLED;
+            } else {
+                int band, pos;
+                plane::pick_cell(und, node_order, band, pos);
+                const uint32_t cand = plane::cell_cand(B, band, pos);
+                const uint32_t d = cand & (0u - cand);
+#pragma unroll
+                for (int w = 0; w < 27; ++w) stk.put(depth, w, B.P[w / 3][w % 3]);
+                stk.put(depth, plane::STACK_ENTRY, plane::make_entry(band, pos, cand ^ d));
+                depth++;
+                guesses += lanes_here();
+                plane::set_cell(B, band, pos, d);
+            }
+        } else if (r == plane::DEAD) {
+            // back to the deepest level with an untried digit
+            for (;;) {
+                if (depth == 0) {
+                    state = PL_UNSOLVABLE;
+                    break;
+                }
+                depth--;
+                const uint32_t e = stk.get(depth, plane::STACK_ENTRY);
+                const uint32_t rem = (e >> 8) & 0x1FFu;
+                if (!rem) continue;
+                const uint32_t d = rem & (0u - rem);
+#pragma unroll
+                for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = stk.get(depth, w);
+                B.Det[0] = B.Det[1] = B.Det[2] = 0;
+                stk.put(depth, plane::STACK_ENTRY, e & ~(d << 8));
+                depth++;
+                guesses += lanes_here();
+                plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
+                break;
+            }
+        }
+    }
+    // per-wave statistics: one atomic per counter and wave
+    if (lane == 0 && deferred) atomicAdd(&ws[WS_DEFERRED], (unsigned long long)deferred);
+    if (lane == 0 && fin) {
+        atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
+        atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
+        atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
+        atomicAdd(&ws[WS_SWEEPS], (unsigned long long)passes);
+    }
+}
+
+#endif  // SDK_PLANE_KERNEL_H

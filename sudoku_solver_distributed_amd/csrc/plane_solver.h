@@ -1,0 +1,383 @@
+// plane_solver.h -- one board per LANE on digit-plane bitboards.
+//
+// Same contract as the wave-per-board kernels (sudoku_kernels.hip): the
+// first completion of the reference walk `order` (gen.py:6-28 /
+// node.py:62-74), found with sound propagation + branching on the walk's
+// next undetermined cell, digits ascending.  The state of a
+// board is nine digit planes: P[d][b] is the set of cells of band b (rows
+// 3b..3b+2) where digit d+1 is still possible, one 32-bit word per band:
+//
+//     bit 10*k + c  = cell (3b+k, c)      k = 0..2, c = 0..8
+//     bits 9, 19, 29 = guard bits (always 0), bits 30-31 unused
+//
+// A cell whose only candidate is d is "determined" (it is the reference's
+// filled cell).  The guard bits let one add / subtract act on the three
+// 9-cell rows of a word at once without carries crossing rows.
+//
+// One pass (pass()) applies, to every cell and unit of the board:
+//   A. determined cells: cells with one candidate; a cell with none is dead;
+//   B. each newly determined cell removes its digit from its row, column and
+//      box (a clash with an older determined cell empties that cell: dead);
+//   C. hidden singles: a digit with exactly one place in a unit goes there;
+//      a digit with no place in a unit kills the node; two digits forced into
+//      one cell kill it.
+// Rules B and C are sound only when the givens do not repeat a digit in a
+// unit (the walk never tests givens, gen.py:8-28): such boards are reported
+// as `bad` by load() and left to the wave-per-board kernel, which handles
+// them.  Two determined cells sharing a digit in one unit are not flagged
+// the moment they appear; the search can only end on a board where every
+// unit holds every digit (pass(): all cells determined and rule C's
+// empty-unit test clean), so such a node still dies, a few passes later.
+//
+// Everything here is plain C++ usable on host and device: the CPU tests
+// compile it with g++ (tests/native/plane_host.cpp) and check it against
+// the oracle before the GPU runs it.
+#ifndef SDK_PLANE_SOLVER_H
+#define SDK_PLANE_SOLVER_H
+
+#include <stdint.h>
+
+#ifdef __HIPCC__
+#define PS_FN __host__ __device__ __forceinline__
+#else
+#define PS_FN static inline
+#endif
+
+#if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+// Make later code consume a value as it stands here (no instruction is
+// emitted).  Pinning the board between the digits of a pass keeps the
+// scheduler from hoisting nine digits' worth of independent work and running
+// the pass at ~130 VGPRs instead of ~60.
+#define PS_PIN(x) asm volatile("" : "+v"(x))
+#else
+#define PS_PIN(x) ((void)0)
+#endif
+
+namespace plane {
+
+enum : uint32_t {
+    ROWS = 0x1FFu | (0x1FFu << 10) | (0x1FFu << 20),  // the 27 cells of a band word
+    GUARDS = (1u << 9) | (1u << 19) | (1u << 29),     // one guard bit above each row
+    ONES = 1u | (1u << 10) | (1u << 20),              // bit 0 of each row
+    KDEC = GUARDS - ONES,                             // y + KDEC == (y | GUARDS) - ONES
+    BOXC = 0x49u,                                     // bit 0 of each 3-column box group
+};
+
+enum { OPEN = 0, DEAD = 1, SOLVED = 2, STUCK = 3 };
+
+struct Board {
+    uint32_t P[9][3];  // P[d][b]: cells of band b where digit d+1 is possible
+    uint32_t Det[3];   // determined cells already eliminated from their peers
+};
+
+PS_FN void pin_board(Board &B)
+{
+#pragma unroll
+    for (int d = 0; d < 9; ++d)
+#pragma unroll
+        for (int b = 0; b < 3; ++b) PS_PIN(B.P[d][b]);
+}
+
+PS_FN constexpr int cell_band(int i) { return i / 27; }
+PS_FN constexpr int cell_pos(int i) { return 10 * ((i / 9) % 3) + i % 9; }
+// cell index of (band, bit position)
+PS_FN int pos_cell(int b, int pos) { return 27 * b + 9 * (pos / 10) + pos % 10; }
+
+PS_FN uint32_t spread_rows(uint32_t c) { return c | (c << 10) | (c << 20); }  // 9-bit column set -> 3 rows
+PS_FN uint32_t guard_rows(uint32_t g) { return g - (g >> 9); }               // guard flags -> whole rows
+PS_FN uint32_t row_nonzero(uint32_t y) { return (y + ROWS) & GUARDS; }        // guard set iff row != 0
+PS_FN uint32_t fold_rows(uint32_t y) { return (y | (y >> 10) | (y >> 20)) & 0x1FFu; }
+
+struct Board;
+PS_FN void pin_board(Board &B);
+
+// One propagation pass (rules A, B, C above).  Returns DEAD, SOLVED, STUCK
+// (a fixpoint: und[] = the undetermined cells, each with >= 2 candidates) or
+// OPEN (something changed: pass again).
+PS_FN int pass(Board &B, uint32_t und[3])
+{
+    uint32_t single[3], nd[3];
+    uint32_t dead = 0;
+    // ---- A: determined cells
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        uint32_t o = 0, t = 0;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            t |= o & B.P[d][b];
+            o |= B.P[d][b];
+        }
+        dead |= ROWS & ~o;
+        single[b] = o & ~t;
+        nd[b] = single[b] & ~B.Det[b];
+        B.Det[b] = single[b];
+        und[b] = ROWS & ~single[b];
+    }
+    const bool all_single = (single[0] & single[1] & single[2]) == ROWS;
+    const bool any_nd = (nd[0] | nd[1] | nd[2]) != 0;
+    pin_board(B);
+
+    uint32_t hall[3] = {0u, 0u, 0u};
+    uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+        // ---- B: remove d from the peers of the newly determined cells holding d
+        uint32_t x[3], f[3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            x[b] = nd[b] & B.P[d][b];
+            f[b] = fold_rows(x[b]);
+        }
+        const uint32_t cpeer = spread_rows(f[0] | f[1] | f[2]);
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t g = f[b] | (f[b] >> 1) | (f[b] >> 2);
+            const uint32_t peer = guard_rows(row_nonzero(x[b])) | cpeer | spread_rows((g & BOXC) * 7u);
+            B.P[d][b] = (peer & x[b]) | (~peer & B.P[d][b]);
+        }
+        // ---- C: hidden singles of d; units with no place left for d
+        uint32_t o[3], t[3], hb[3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t y = B.P[d][b];
+            const uint32_t nzy = row_nonzero(y);
+            const uint32_t nzm = row_nonzero(y & (y + KDEC));  // rows with >= 2 places
+            rowall &= nzy;
+            const uint32_t hr = y & guard_rows(nzy & ~nzm);
+            const uint32_t s1 = y >> 10, s2 = y >> 20;
+            o[b] = (y | s1 | s2) & 0x1FFu;                        // per column: >= 1 place in the band
+            t[b] = ((y & s1) | (s2 & (y | s1))) & 0x1FFu;        // per column: >= 2 places in the band
+            const uint32_t o1 = o[b] >> 1, o2 = o[b] >> 2;
+            const uint32_t ob = o[b] | o1 | o2;                   // per box (bits 0, 3, 6)
+            const uint32_t tb = t[b] | (t[b] >> 1) | (t[b] >> 2) | (o[b] & o1) | (o2 & (o[b] | o1));
+            boxall &= ob;
+            hb[b] = hr | (y & spread_rows((ob & ~tb & BOXC) * 7u));
+        }
+        const uint32_t O = o[0] | o[1] | o[2];
+        const uint32_t T = t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
+        colall &= O;
+        const uint32_t hcol = spread_rows(O & ~T);
+        // place d's hidden singles at once (Gauss-Seidel: later digits see
+        // them).  A cell forced for two digits loses the later one, whose
+        // unit then has no place for it: dead, as it must be.
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t h = hb[b] | (B.P[d][b] & hcol);
+            hall[b] |= h;
+#pragma unroll
+            for (int e = 0; e < 9; ++e)
+                if (e != d) B.P[e][b] &= ~h;
+        }
+        pin_board(B);
+    }
+    dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
+    if (dead) return DEAD;
+    if (all_single) return SOLVED;
+    const bool newh = ((hall[0] & und[0]) | (hall[1] & und[1]) | (hall[2] & und[2])) != 0;
+    return (any_nd || newh) ? OPEN : STUCK;
+}
+
+// The walk's branch cell among the undetermined cells: node.py:63-65 takes
+// the first in row-major order; gen.py:11-15 the first of the LAST row that
+// has one (its column loop breaks, its row loop does not).
+PS_FN void pick_cell(const uint32_t und[3], int node_order, int &band, int &pos)
+{
+    if (node_order) {
+        band = und[0] ? 0 : und[1] ? 1 : 2;
+        const uint32_t w = band == 0 ? und[0] : band == 1 ? und[1] : und[2];
+        pos = __builtin_ctz(w);
+    } else {
+        band = und[2] ? 2 : und[1] ? 1 : 0;
+        const uint32_t w = band == 0 ? und[0] : band == 1 ? und[1] : und[2];
+        const int hi = 31 - __builtin_clz(w);
+        const int k = hi >= 20 ? 2 : hi >= 10 ? 1 : 0;
+        pos = 10 * k + __builtin_ctz(w >> (10 * k));
+    }
+}
+
+PS_FN uint32_t band_word(const uint32_t (&w)[3], int band) { return band == 0 ? w[0] : band == 1 ? w[1] : w[2]; }
+
+// candidates (bit d = digit d+1) of the cell at (band, pos)
+PS_FN uint32_t cell_cand(const Board &B, int band, int pos)
+{
+    uint32_t c = 0;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) c |= ((band_word(B.P[d], band) >> pos) & 1u) << d;
+    return c;
+}
+
+// fix the cell at (band, pos) to the digit bit `dbit` (bit d = digit d+1)
+PS_FN void set_cell(Board &B, int band, int pos, uint32_t dbit)
+{
+    const uint32_t cb = 1u << pos;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+        const uint32_t clr = ((dbit >> d) & 1u) ? 0u : cb;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) B.P[d][b] &= (b == band) ? ~clr : ~0u;
+    }
+}
+
+// ---------------------------------------------------------- load / store
+// Value bit-slices -> planes.  V[s][b]: cells whose value has bit s set;
+// E[b]: empty cells.  Returns the given cells (non-empty).
+PS_FN void planes_from_slices(Board &B, const uint32_t (&V)[4][3], uint32_t (&given)[3])
+{
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        const uint32_t v0 = V[0][b], v1 = V[1][b], v2 = V[2][b], v3 = V[3][b];
+        const uint32_t n0 = ROWS & ~v0, n1 = ROWS & ~v1, n2 = ROWS & ~v2, n3 = ROWS & ~v3;
+        const uint32_t e = n0 & n1 & n2 & n3;
+        given[b] = ROWS & ~e;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const int v = d + 1;
+            const uint32_t eq = ((v & 1) ? v0 : n0) & ((v & 2) ? v1 : n1) & ((v & 4) ? v2 : n2) & ((v & 8) ? v3 : n3);
+            B.P[d][b] = eq | e;
+        }
+        B.Det[b] = 0;
+    }
+}
+
+// Do the givens repeat a digit in some row, column or box?  (Such boards
+// are legal input -- the walk never tests the givens -- but rules B/C are
+// unsound on them; the caller hands them to the wave-per-board kernel.)
+PS_FN bool givens_clash(const Board &B, const uint32_t (&given)[3])
+{
+    uint32_t bad = 0;
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+        uint32_t o[3], t[3];
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t y = B.P[d][b] & given[b];
+            bad |= y & (y + KDEC);  // a row with two
+            const uint32_t s1 = y >> 10, s2 = y >> 20;
+            o[b] = (y | s1 | s2) & 0x1FFu;
+            t[b] = ((y & s1) | (s2 & (y | s1))) & 0x1FFu;
+            const uint32_t o1 = o[b] >> 1, o2 = o[b] >> 2;
+            bad |= (t[b] | (t[b] >> 1) | (t[b] >> 2) | (o[b] & o1) | (o2 & (o[b] | o1))) & BOXC;
+        }
+        bad |= t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
+    }
+    return bad != 0;
+}
+
+// Load from 21 words x[k] = bytes 4k..4k+3 of the board (little endian; only
+// byte 80 of x[20] is used).  Returns false if a byte is > 9.
+PS_FN bool load_words(Board &B, const uint32_t (&x)[21], bool &clash)
+{
+    uint32_t V[4][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}};
+    uint32_t badb = 0;
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+        const uint32_t w = k == 20 ? (x[k] & 0xFFu) : x[k];
+        badb |= ((w & 0x7F7F7F7Fu) + 0x76767676u | w) & 0x80808080u;  // some byte > 9
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int i = 4 * k + j;
+            if (i > 80) break;
+            const int b = cell_band(i), p = cell_pos(i);
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const int src = 8 * j + s;
+                const uint32_t bit = p >= src ? (w << (p - src)) : (w >> (src - p));
+                V[s][b] |= bit & (1u << p);
+            }
+        }
+        // one word at a time: unpinned, the OR chains of all 81 cells are
+        // re-associated into trees that keep every shifted term live
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) PS_PIN(V[s][b]);
+        PS_PIN(badb);
+    }
+    uint32_t given[3];
+    planes_from_slices(B, V, given);
+    clash = badb == 0 && givens_clash(B, given);
+    return badb == 0;
+}
+
+// Store a SOLVED board: one byte per cell through `put(i, value)`.
+template <typename Put>
+PS_FN void store_values(const Board &B, Put put)
+{
+    uint32_t V[4][3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        const uint32_t p0 = B.P[0][b], p1 = B.P[1][b], p2 = B.P[2][b], p3 = B.P[3][b], p4 = B.P[4][b];
+        const uint32_t p5 = B.P[5][b], p6 = B.P[6][b], p7 = B.P[7][b], p8 = B.P[8][b];
+        V[0][b] = p0 | p2 | p4 | p6 | p8;  // digits 1 3 5 7 9
+        V[1][b] = p1 | p2 | p5 | p6;       // 2 3 6 7
+        V[2][b] = p3 | p4 | p5 | p6;       // 4 5 6 7
+        V[3][b] = p7 | p8;                 // 8 9
+    }
+#pragma unroll
+    for (int i = 0; i < 81; ++i) {
+        const int b = cell_band(i), p = cell_pos(i);
+        const uint32_t v = ((V[0][b] >> p) & 1u) | (((V[1][b] >> p) & 1u) << 1) | (((V[2][b] >> p) & 1u) << 2) |
+                           (((V[3][b] >> p) & 1u) << 3);
+        put(i, v);
+    }
+}
+
+// stack level: the 27 plane words + the branch entry
+enum { STACK_WORDS = 28, STACK_ENTRY = 27 };
+// branch entry: bits 0-4 pos, 5-6 band, 8-16 untried digits
+PS_FN uint32_t make_entry(int band, int pos, uint32_t rem) { return (uint32_t)pos | ((uint32_t)band << 5) | (rem << 8); }
+
+// Host / reference driver: solve one board in place with a stack of at
+// least max_depth levels.  Returns 1 solved, 0 no completion, -1 depth
+// overflow (board left to the wave kernel).
+struct Stats {
+    uint32_t guesses, passes;
+};
+
+template <typename Stack>
+PS_FN int solve(Board &B, Stack &stk, int node_order, uint32_t max_depth, Stats &st)
+{
+    uint32_t depth = 0;
+    for (;;) {
+        uint32_t und[3];
+        const int r = pass(B, und);
+        st.passes++;
+        if (r == SOLVED) return 1;
+        if (r == OPEN) continue;
+        if (r == STUCK) {
+            if (depth == max_depth) return -1;
+            int band, pos;
+            pick_cell(und, node_order, band, pos);
+            const uint32_t cand = cell_cand(B, band, pos);
+            const uint32_t d = cand & (0u - cand);
+#pragma unroll
+            for (int w = 0; w < 27; ++w) stk.put(depth, w, B.P[w / 3][w % 3]);
+            stk.put(depth, STACK_ENTRY, make_entry(band, pos, cand ^ d));
+            depth++;
+            st.guesses++;
+            set_cell(B, band, pos, d);
+            continue;
+        }
+        // DEAD: back to the deepest level with an untried digit
+        for (;;) {
+            if (depth == 0) return 0;
+            depth--;
+            const uint32_t e = stk.get(depth, STACK_ENTRY);
+            const uint32_t rem = (e >> 8) & 0x1FFu;
+            if (!rem) continue;
+            const uint32_t d = rem & (0u - rem);
+#pragma unroll
+            for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = stk.get(depth, w);
+            B.Det[0] = B.Det[1] = B.Det[2] = 0;
+            stk.put(depth, STACK_ENTRY, e & ~(d << 8));
+            depth++;
+            st.guesses++;
+            set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
+            break;
+        }
+    }
+}
+
+}  // namespace plane
+
+#endif  // SDK_PLANE_SOLVER_H

@@ -42,66 +42,12 @@
 #include "../../include/sudoku_hip.h"
 #include "lane_solver.h"
 
-#define WAVES_PER_BLOCK 4
-#define BLOCK_THREADS (64 * WAVES_PER_BLOCK)
+#include "common.h"
 
-// ---------------------------------------------------------------- workspace
-// word layout of the device workspace (uint64 words)
-enum {
-    WS_QUEUE = 0,      // chunked board queue head (re-armed every call)
-    WS_BEST = 1,       // ordered mode: lowest solved index (re-armed to INT64_MAX)
-    WS_ARM_WORDS = 2,  // words re-armed per call
-    WS_FINISHED = 8,   // statistics (accumulate until sdk_read_stats(reset))
-    WS_SOLVED = 9,
-    WS_GUESSES = 10,
-    WS_SWEEPS = 11,
-    WS_WORDS = 16
-};
-
-struct __attribute__((aligned(16))) WaveLds {
-    uint32_t M[28];  // unit masks of filled cells (rows 0-8, columns 9-17, boxes 18-26)
-    uint32_t T[28];  // per unit: digits that are candidates of >= 2 of its empty cells
-    uint32_t C[128]; // per cell: candidate mask published for the unit gather (0 = filled; 81.. padding)
-    uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
-    uint32_t pad[3];
-};
-
-__device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
-
-// Orders this wave's LDS accesses (a single wave's DS ops execute in order;
-// this keeps the compiler from moving them and drains returns).
-__device__ __forceinline__ void wave_lds_sync()
-{
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
-    __builtin_amdgcn_wave_barrier();
-}
-
-// Order this wave's LDS accesses for the compiler only.  A wavefront's DS
-// instructions execute in issue order, so a lane's read issued after another
-// lane's write/atomic of the same word sees it without waiting for the
-// write's return: the sweep's round trips (atomics -> mask reads, publish ->
-// gather -> T reads) overlap in the LDS pipeline instead of each draining
-// lgkmcnt.  The signal fence keeps the compiler from moving accesses across.
-#ifndef SDK_LDS_INORDER
-#define SDK_LDS_INORDER 0
+#ifndef SDK_PLANE_MIN_BATCH
+#define SDK_PLANE_MIN_BATCH 8192
 #endif
-__device__ __forceinline__ void wave_lds_order()
-{
-#if SDK_LDS_INORDER
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#else
-    wave_lds_sync();
-#endif
-}
 
-// wave-uniform "any lane": the ballot's SGPR pair, no VGPR round trip
-__device__ __forceinline__ bool wany(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
-
-__device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
 
 // Per-lane view of its two cells, plus the lane's unit role (lanes 0..26).
 struct Cells {
@@ -1320,19 +1266,39 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
     cached.store(nb);
     return nb;
 }
-static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0}, g_bpc_v4{0};
+static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0}, g_bpc_v4{0}, g_bpc_plane{0};
 
-// kernel variant: 5 = one board per wave, packed cell pairs (default);
-// 2 = one board per wave, one register set per cell slot (SDK_SOLVE_KERNEL=2);
-// 3 = two boards per wave (=3), 4 = one board per lane (=l): measured slower
-// on MI355X, see DESIGN.md
+// lanes of a full plane-kernel grid on the current device, and the bytes of
+// their stacks (the workspace holds them after WS_STACK_BYTE)
+static int64_t plane_max_threads()
+{
+    if (!g_bpc_plane.load()) g_bpc_plane.store(sdk_plane_blocks_per_cu());
+    return (int64_t)cu_count() * g_bpc_plane.load() * PLANE_THREADS;
+}
+static size_t plane_stack_bytes(int64_t threads)
+{
+    return (size_t)threads * PLANE_MAX_DEPTH * PLANE_STACK_WORDS * sizeof(uint32_t);
+}
+
+// kernel variant: 1 = auto (default): 6 for batches of at least
+// SDK_PLANE_MIN_BATCH boards, 5 below (a lone board on one lane is slower
+// than on a whole wave, and a small batch does not fill the lanes);
+// 6 = one board per lane on digit planes (SDK_SOLVE_KERNEL=plane);
+// 5 = one board per wave, packed cell pairs (SDK_SOLVE_KERNEL=p);
+// 2 = one board per wave, one register set per cell slot (=2);
+// 3 = two boards per wave (=3), 4 = one board per lane, nibble cells (=l).
+// All give identical results; DESIGN.md has the measurements.
 static std::atomic<int> g_variant{0};
 
 static int env_variant()
 {
     const char *e = getenv("SDK_SOLVE_KERNEL");
-    return (e && e[0] == '3') ? SDK_KERNEL_PAIR : (e && e[0] == 'l') ? SDK_KERNEL_LANE
-         : (e && (e[0] == '2' || e[0] == 'w')) ? SDK_KERNEL_WAVE : SDK_KERNEL_PACKED;
+    if (!e || !e[0] || e[0] == 'a') return SDK_KERNEL_AUTO;
+    if (e[0] == '3') return SDK_KERNEL_PAIR;
+    if (e[0] == 'l') return SDK_KERNEL_LANE;
+    if (e[0] == '2' || e[0] == 'w') return SDK_KERNEL_WAVE;
+    if (e[0] == 'p' && e[1] != 'l') return SDK_KERNEL_PACKED;
+    return SDK_KERNEL_PLANE;
 }
 
 static int solve_variant()
@@ -1351,7 +1317,9 @@ const char *sdk_last_error(void) { return g_err; }
 const char *sdk_version(void)
 {
     const int v = solve_variant();
-    return v == SDK_KERNEL_LANE ? "sudoku_hip 0.3 gfx950 lane-per-board walk-order"
+    return v == SDK_KERNEL_AUTO ? "sudoku_hip 0.5 gfx950 auto: lane-per-board digit-planes (large batches), wave-per-board packed-pairs (small) walk-order"
+         : v == SDK_KERNEL_PLANE ? "sudoku_hip 0.5 gfx950 lane-per-board digit-planes walk-order"
+         : v == SDK_KERNEL_LANE ? "sudoku_hip 0.3 gfx950 lane-per-board walk-order"
          : v == SDK_KERNEL_PACKED ? "sudoku_hip 0.4 gfx950 wave-per-board packed-pairs walk-order"
          : v == SDK_KERNEL_PAIR ? "sudoku_hip 0.3 gfx950 board-pair-per-wave walk-order"
                   : "sudoku_hip 0.3 gfx950 wave-per-board walk-order";
@@ -1360,13 +1328,13 @@ int sdk_device_cu_count(void) { return cu_count(); }
 int sdk_set_solve_kernel(int kernel)
 {
     if (kernel != 0 && kernel != SDK_KERNEL_WAVE && kernel != SDK_KERNEL_PAIR && kernel != SDK_KERNEL_LANE &&
-        kernel != SDK_KERNEL_PACKED)
+        kernel != SDK_KERNEL_PACKED && kernel != SDK_KERNEL_PLANE && kernel != SDK_KERNEL_AUTO)
         return -1;
     const int prev = solve_variant();
     g_variant.store(kernel ? kernel : env_variant());
     return prev;
 }
-size_t sdk_workspace_bytes(void) { return WS_WORDS * sizeof(unsigned long long); }
+size_t sdk_workspace_bytes(void) { return WS_STACK_BYTE + plane_stack_bytes(plane_max_threads()); }
 
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
                     void *d_workspace, int order, int ordered, void *stream)
@@ -1381,7 +1349,8 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     unsigned long long *ws = (unsigned long long *)d_workspace;
     hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     hipError_t e;
-    const int variant = solve_variant();
+    int variant = solve_variant();
+    if (variant == SDK_KERNEL_AUTO) variant = n >= SDK_PLANE_MIN_BATCH ? SDK_KERNEL_PLANE : SDK_KERNEL_PACKED;
     if (variant == SDK_KERNEL_LANE) {
         // lane per board: one persistent thread per resident lane
         const int64_t max_threads = (int64_t)cu_count() * blocks_per_cu(lane_kernel, g_bpc_lane) * BLOCK_THREADS;
@@ -1412,6 +1381,19 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
         const int64_t blocks = (waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK;
         hipLaunchKernelGGL(solvep_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
                            d_status, n, ws, chunk, ordered, order);
+    } else if (variant == SDK_KERNEL_PLANE) {
+        // lanes: one per board up to a full grid; the stacks sit in the workspace
+        const int64_t max_threads = plane_max_threads();
+        const int64_t threads = n < max_threads ? n : max_threads;
+        uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
+        e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, ordered, order, threads, st);
+        if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
+        // the boards it left (clashing givens, deep searches): wave per board
+        const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_deferred_kernel, g_bpc_v4) * WAVES_PER_BLOCK;
+        const int64_t groups = (n + 63) / 64;
+        const int64_t waves = groups < max_waves ? groups : max_waves;
+        hipLaunchKernelGGL(solvep_deferred_kernel, dim3((unsigned)((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
+                           dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions, d_status, n, ws, ordered, order);
     } else {
         const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solve_kernel, g_bpc_v2) * WAVES_PER_BLOCK;
         const int64_t waves = n < max_waves ? n : max_waves;
@@ -1494,9 +1476,9 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
     out[2] = (int64_t)h[WS_GUESSES];
     out[3] = (int64_t)h[WS_SWEEPS];
     out[4] = (int64_t)h[WS_BEST];
-    out[5] = 0;
+    out[5] = (int64_t)h[WS_DEFERRED];
     if (reset) {
-        e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 4 * sizeof(unsigned long long), st);
+        e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 5 * sizeof(unsigned long long), st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return set_err("sdk_read_stats: reset", e);
     }

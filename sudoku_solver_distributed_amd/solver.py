@@ -153,7 +153,8 @@ class BatchSolver:
         with torch.cuda.device(self.device):
             rc = self.lib.sdk_read_stats(self.workspace.data_ptr(), out, 1 if reset else 0, self._stream(stream))
         _lib.check(rc, "sdk_read_stats")
-        return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4]}
+        return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4],
+                "deferred": out[5]}
 
     # ------------------------------------------------------ frontier split
     def frontier(self, board, target: int = 4096, max_levels: int = 81, order="gen") -> torch.Tensor:

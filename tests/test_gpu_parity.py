@@ -254,7 +254,7 @@ def test_distributed_single_rank_gpu(solver):
     assert np.array_equal(sols.cpu().numpy(), w)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "pair", "lane", "packed"])
+@pytest.mark.parametrize("kernel", ["wave", "pair", "lane", "packed", "plane"])
 def test_alternate_kernels_parity(solver, kernel):
     """The non-default solve kernels (sdk_set_solve_kernel): goldens, generated
     boards in both walks, clashing givens, invalid bytes, ordered mode and
