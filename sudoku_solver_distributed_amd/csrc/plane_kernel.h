@@ -82,7 +82,7 @@ enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLE
 __device__ __forceinline__ uint32_t lanes_here() { return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)); }
 
 #ifndef SDK_PLANE_WAVES_PER_EU
-#define SDK_PLANE_WAVES_PER_EU 2
+#define SDK_PLANE_WAVES_PER_EU 4
 #endif
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
@@ -168,8 +168,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     m &= m - 1;
                     fin++;
                     const uint8_t *src = puzzles + q * 81;
-                    const uint32_t a0 = c0 >= 0 ? src[c0] : 0xFFu, a1 = c1 >= 0 ? src[c1] : 0xFFu;
-                    if (__builtin_amdgcn_ballot_w64((a0 > 9 && a0 != 0xFFu) || (a1 > 9 && a1 != 0xFFu))) {
+                    // slots holding no cell read the sentinel 0x100 (no byte value)
+                    const uint32_t a0 = c0 >= 0 ? src[c0] : 0x100u, a1 = c1 >= 0 ? src[c1] : 0x100u;
+                    if (__builtin_amdgcn_ballot_w64((a0 > 9 && a0 != 0x100u) || (a1 > 9 && a1 != 0x100u))) {
                         plane_copy_board(src, sols + q * 81, lane);  // raw input back
                         if (lane == 0) status[q] = SDK_INVALID;
                         continue;

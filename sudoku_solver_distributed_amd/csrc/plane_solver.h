@@ -169,6 +169,14 @@ PS_FN int pass(Board &B, uint32_t und[3])
                 if (e != d) B.P[e][b] &= ~h;
         }
         pin_board(B);
+        // the unit accumulators too: unpinned, the AND / OR chains over the
+        // nine digits are re-associated into trees at the end of the pass,
+        // keeping 27 row-test words live (~200 VGPRs instead of ~100)
+        PS_PIN(rowall);
+        PS_PIN(colall);
+        PS_PIN(boxall);
+#pragma unroll
+        for (int b = 0; b < 3; ++b) PS_PIN(hall[b]);
     }
     dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;
