@@ -11,8 +11,11 @@ import sys
 _HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(_HERE)
 # translation units and their extra flags (plane_kernels.hip: see its header)
+# SDK_PLANE_SCHED: machine-scheduler strategy of the plane kernel's unit
+# ("default" = LLVM's own; A/B builds)
+_SCHED = os.environ.get("SDK_PLANE_SCHED", "default")
 SRCS = (("sudoku_kernels.hip", []),
-        ("plane_kernels.hip", ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"]))
+        ("plane_kernels.hip", [] if _SCHED == "default" else ["-mllvm", f"-amdgpu-sched-strategy={_SCHED}"]))
 OUT = os.path.join(_HERE, "libsudoku_hip.so")
 ARCH = os.environ.get("SDK_OFFLOAD_ARCH", "gfx950")
 

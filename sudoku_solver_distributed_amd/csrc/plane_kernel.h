@@ -20,8 +20,10 @@
 // atomic queue head per wave refill.
 //
 // Boards the planes cannot take -- givens that repeat a digit in a unit
-// (rules B/C are unsound there, plane_solver.h) or a search deeper than
-// PLANE_MAX_DEPTH -- get status SDK_DEFERRED and no output; the packed
+// (rules B/C are unsound there, plane_solver.h; tested only once a board's
+// search ends without a completion, since a completion proves the givens
+// clean) or a search deeper than PLANE_MAX_DEPTH -- get status SDK_DEFERRED
+// and no output; the packed
 // kernel then runs over the batch with deferred_only set and solves exactly
 // those.  Results are identical either way.
 #ifndef SDK_PLANE_KERNEL_H
@@ -30,7 +32,12 @@
 #include "plane_solver.h"
 
 #ifndef SDK_PLANE_REFILL
-#define SDK_PLANE_REFILL 8
+#define SDK_PLANE_REFILL 12
+#endif
+// 1: test givens for repeated digits only when a search ends without a
+// completion (0: on every load, A/B)
+#ifndef SDK_PLANE_LAZY_CLASH
+#define SDK_PLANE_LAZY_CLASH 1
 #endif
 static_assert(PLANE_STACK_WORDS == plane::STACK_WORDS, "stack layout");
 
@@ -73,6 +80,28 @@ __device__ __forceinline__ void plane_copy_board(const uint8_t *__restrict__ src
 {
     dst[lane] = src[lane];
     if (lane < 17) dst[64 + lane] = src[64 + lane];
+}
+
+// Do board src's givens repeat a digit in a unit?  Wave-cooperative (the
+// ballots make its planes wave-uniform); run only for boards the planes
+// found unsolvable, which is rare.
+__device__ __forceinline__ bool plane_givens_clash(const uint8_t *__restrict__ src, int c0, int c1)
+{
+    const uint32_t a0 = c0 >= 0 ? src[c0] : 0x100u, a1 = c1 >= 0 ? src[c1] : 0x100u;
+    plane::Board G;
+    uint32_t given[3];
+    const uint64_t e0 = __builtin_amdgcn_ballot_w64(a0 == 0u);
+    const uint32_t E[3] = {(uint32_t)e0, (uint32_t)(e0 >> 32), (uint32_t)__builtin_amdgcn_ballot_w64(a1 == 0u)};
+#pragma unroll
+    for (int d = 0; d < 9; ++d) {
+        const uint64_t m0 = __builtin_amdgcn_ballot_w64(a0 == (uint32_t)(d + 1));
+        G.P[d][0] = (uint32_t)m0;
+        G.P[d][1] = (uint32_t)(m0 >> 32);
+        G.P[d][2] = (uint32_t)__builtin_amdgcn_ballot_w64(a1 == (uint32_t)(d + 1));
+    }
+#pragma unroll
+    for (int b = 0; b < 3; ++b) given[b] = plane::ROWS & ~E[b];
+    return plane::givens_clash(G, given);
 }
 
 // lane states; the two "original" states store the input board back
@@ -146,8 +175,19 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 const int i = __builtin_ctzll(m);
                 m &= m - 1;
                 const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                const bool cancelled = rdlane((uint32_t)state, i) == PL_CANCELLED;
+                if (!cancelled && plane_givens_clash(puzzles + pi * 81, c0, c1)) {
+                    // rules B/C are unsound on givens that repeat a digit in a
+                    // unit: "no completion" is the packed kernel's call.  (A
+                    // SOLVED result needs every unit to hold every digit, so
+                    // such givens never reach the store above.)
+                    if (lane == 0) status[pi] = SDK_DEFERRED;
+                    fin--;
+                    deferred++;
+                    continue;
+                }
                 plane_copy_board(puzzles + pi * 81, sols + pi * 81, lane);
-                if (lane == 0) status[pi] = rdlane((uint32_t)state, i) == PL_CANCELLED ? SDK_CANCELLED : SDK_UNSOLVABLE;
+                if (lane == 0) status[pi] = cancelled ? SDK_CANCELLED : SDK_UNSOLVABLE;
             }
             if (state != PL_ACTIVE) state = PL_IDLE;
             // ---- refill the free lanes: one queue add per wave, then one
@@ -160,8 +200,10 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)k);
                 base = __shfl(base, leader);
                 drained = (int64_t)base + k >= n;
-                uint32_t given[3] = {0u, 0u, 0u};
                 bool loaded = false;
+#if !SDK_PLANE_LAZY_CLASH
+                uint32_t given[3] = {0u, 0u, 0u};
+#endif
                 m = idle;
                 for (int64_t q = (int64_t)base; m && q < n; ++q) {
                     const int i = __builtin_ctzll(m);
@@ -192,15 +234,20 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                         B.P[d][2] = lane == i ? (m1 | E[2]) : B.P[d][2];
                     }
                     if (lane == i) {
+#if !SDK_PLANE_LAZY_CLASH
 #pragma unroll
                         for (int b = 0; b < 3; ++b) given[b] = plane::ROWS & ~E[b];
+#endif
                         B.Det[0] = B.Det[1] = B.Det[2] = 0;
                         p = q;
                         depth = 0;
                         loaded = true;
                     }
                 }
-                // givens repeating a digit in a unit: the packed kernel's board
+#if SDK_PLANE_LAZY_CLASH
+                if (loaded) state = PL_ACTIVE;
+#else
+                // eager variant (A/B): every loaded board's givens, lane-parallel
                 if (loaded) {
                     if (plane::givens_clash(B, given)) {
                         status[p] = SDK_DEFERRED;
@@ -211,6 +258,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                         state = PL_ACTIVE;
                     }
                 }
+#endif
             }
             if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;
         }

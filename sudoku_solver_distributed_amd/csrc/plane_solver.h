@@ -52,6 +52,9 @@
 #else
 #define PS_PIN(x) ((void)0)
 #endif
+#ifndef SDK_PLANE_PIN_ACC
+#define SDK_PLANE_PIN_ACC 1
+#endif
 
 namespace plane {
 
@@ -172,11 +175,13 @@ PS_FN int pass(Board &B, uint32_t und[3])
         // the unit accumulators too: unpinned, the AND / OR chains over the
         // nine digits are re-associated into trees at the end of the pass,
         // keeping 27 row-test words live (~200 VGPRs instead of ~100)
+#if SDK_PLANE_PIN_ACC
         PS_PIN(rowall);
         PS_PIN(colall);
         PS_PIN(boxall);
 #pragma unroll
         for (int b = 0; b < 3; ++b) PS_PIN(hall[b]);
+#endif
     }
     dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;

@@ -131,11 +131,23 @@ def test_invalid_bytes_rejected(solver):
     assert int(sols[1, 5]) == 12
 
 
+@pytest.mark.parametrize("kernel", ["auto", "plane"])
 @pytest.mark.parametrize("order", ["gen", "node"])
-def test_duplicate_givens_vs_oracle(solver, order):
+def test_duplicate_givens_vs_oracle(solver, order, kernel):
     """Clashing givens: the walk never tests givens, so such boards can still
     be completed (e.g. nearly full boards); compare where a completion exists
-    and the board is otherwise unchanged-False."""
+    and the board is otherwise unchanged-False.  `plane` forces the
+    lane-per-board kernel, which tests for clashing givens only once a search
+    ends without a completion and then defers the board."""
+    from sudoku_solver_distributed_amd import _lib
+    prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
+    try:
+        _duplicate_givens_case(solver, order)
+    finally:
+        solver.lib.sdk_set_solve_kernel(prev)
+
+
+def _duplicate_givens_case(solver, order):
     rng = np.random.default_rng(3)
     from sudoku_solver_distributed_amd.gen import generate_batch
     full = generate_batch(300, 0, seed=77).cpu().numpy()
