@@ -11,7 +11,7 @@ timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun
 rc=$?; tail -2 gpurun_out/smoke.log; step smoke $rc
 timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
 rc=$?; tail -c 600 gpurun_out/bench.json; step bench $rc
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python -u bench.py --no-cpu > gpurun_out/prof_trace.log 2>&1
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python -u bench.py --no-cpu --no-extras --latency-boards 0 > gpurun_out/prof_trace.log 2>&1
 step trace $?
 bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1
 step pmc $?
