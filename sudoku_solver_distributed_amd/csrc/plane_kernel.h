@@ -39,6 +39,10 @@
 #ifndef SDK_PLANE_LAZY_CLASH
 #define SDK_PLANE_LAZY_CLASH 1
 #endif
+// 1: each lane loads its own first board (lane-parallel start-up)
+#ifndef SDK_PLANE_LANE_START
+#define SDK_PLANE_LANE_START 1
+#endif
 static_assert(PLANE_STACK_WORDS == plane::STACK_WORDS, "stack layout");
 
 // Per-lane stack in the workspace: word w of level L of lane g lives at
@@ -107,6 +111,11 @@ __device__ __forceinline__ bool plane_givens_clash(const uint8_t *__restrict__ s
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
+__device__ __forceinline__ unsigned long long rdlane64(unsigned long long v, int l)
+{
+    return ((unsigned long long)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
+}
+
 // number of lanes executing this point (the exec mask of a divergent branch)
 __device__ __forceinline__ uint32_t lanes_here() { return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)); }
 
@@ -133,6 +142,41 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // wave-uniform statistics
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     bool drained = false;  // the queue is empty
+
+#if SDK_PLANE_LANE_START
+    // Start-up: every lane loads its own first board, all lanes and all 81
+    // byte loads at once.  The cooperative refill below loads one board per
+    // HBM round trip, which for a wave's first 64 boards is ~10 passes' time.
+    {
+        unsigned long long base = 0;
+        if (lane == 0) base = atomicAdd(&ws[WS_QUEUE], 64ull);
+        base = rdlane64(base, 0);
+        drained = (int64_t)base + 64 >= n;
+        const int64_t q = (int64_t)base + lane;
+        if (q < n) {
+            fin += lanes_here();
+            const uint8_t *src = puzzles + q * 81;
+            uint32_t x[21];
+#pragma unroll
+            for (int k = 0; k < 21; ++k) {
+                uint32_t w = src[4 * k];
+                if (k < 20) w |= ((uint32_t)src[4 * k + 1] << 8) | ((uint32_t)src[4 * k + 2] << 16) | ((uint32_t)src[4 * k + 3] << 24);
+                x[k] = w;
+            }
+            bool clash;  // tested lazily (see the unsolvable store above)
+            const bool ok = plane::load_words(B, x, clash);
+            const bool cancel = ok && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q;
+            if (ok && !cancel) {
+                p = q;
+                depth = 0;
+                state = PL_ACTIVE;
+            } else {
+                for (int i = 0; i < 81; ++i) sols[q * 81 + i] = src[i];  // raw input back
+                status[q] = ok ? SDK_CANCELLED : SDK_INVALID;
+            }
+        }
+    }
+#endif
 
     for (;;) {
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);

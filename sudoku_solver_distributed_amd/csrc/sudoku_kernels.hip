@@ -1270,6 +1270,19 @@ static std::atomic<int> g_bpc_v2{0}, g_bpc_v3{0}, g_bpc_lane{0}, g_bpc_v4{0}, g_
 
 // lanes of a full plane-kernel grid on the current device, and the bytes of
 // their stacks (the workspace holds them after WS_STACK_BYTE)
+#ifndef SDK_PLANE_BOARDS_PER_LANE
+#define SDK_PLANE_BOARDS_PER_LANE 0
+#endif
+// SDK_PLANE_BPL overrides the default (A/B runs)
+static int64_t plane_boards_per_lane()
+{
+    static const int64_t v = [] {
+        const char *e = getenv("SDK_PLANE_BPL");
+        return e && e[0] ? (int64_t)atoll(e) : (int64_t)SDK_PLANE_BOARDS_PER_LANE;
+    }();
+    return v;
+}
+
 static int64_t plane_max_threads()
 {
     if (!g_bpc_plane.load()) g_bpc_plane.store(sdk_plane_blocks_per_cu());
@@ -1384,7 +1397,16 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     } else if (variant == SDK_KERNEL_PLANE) {
         // lanes: one per board up to a full grid; the stacks sit in the workspace
         const int64_t max_threads = plane_max_threads();
-        const int64_t threads = n < max_threads ? n : max_threads;
+        int64_t threads = n < max_threads ? n : max_threads;
+        // at least plane_boards_per_lane() boards per lane: with too few, the
+        // drain at the end of the batch (lanes idle while their wave's last
+        // boards finish) dominates the launch
+        const int64_t bpl = plane_boards_per_lane();
+        if (bpl > 1 && threads > n / bpl) {
+            threads = n / bpl;
+            threads = threads < PLANE_THREADS ? PLANE_THREADS : (threads + PLANE_THREADS - 1) / PLANE_THREADS * PLANE_THREADS;
+            if (threads > max_threads) threads = max_threads;
+        }
         uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
         e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, ordered, order, threads, st);
         if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
