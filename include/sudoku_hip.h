@@ -38,17 +38,22 @@ extern "C" {
 
 /* Bytes of device workspace sdk_solve_batch needs on the current device:
  * queue heads, cancel word, statistics, and the plane kernel's per-lane DFS
- * stacks (about 1.5 GB on an MI355X).  Allocate once per device and stream,
- * zero once; the library re-arms the per-call words itself on `stream`. */
+ * stacks (about 0.94 GB on an MI355X).  Allocate once per device, zero once;
+ * the library re-arms the per-call words itself on `stream`.
+ * A workspace is SINGLE-STREAM: every call that passes the same workspace
+ * must be issued on the same stream (or ordered by the caller), because each
+ * sdk_solve_batch re-arms the workspace's queue head before its kernels.
+ * Enqueueing is thread-safe (the library serialises its launch sequences). */
 size_t sdk_workspace_bytes(void);
 
 /* Solve n boards.  For every board the output is the FIRST solution of the
- * reference walk selected by `order`:
+ * reference walk selected by `order`, bit-identical:
  *   SDK_ORDER_GEN  gen.py:6-28          solve_sudoku(board)
- *   SDK_ORDER_NODE node.py:31-40,62-74  SudokuSolver.solve_sudoku
- * bit-identical (node.py additionally short-circuits is_valid_move on boards
- * whose every unit already sums to 45 -- only boards with clashing givens
- * can reach that).  d_puzzles and d_solutions may alias.
+ *   SDK_ORDER_NODE node.py:31-40,62-74  SudokuSolver.solve_sudoku, including
+ *                  is_valid_move's short-circuit (node.py:44-45: every unit
+ *                  sums to 45 -> any digit is accepted; only boards with
+ *                  clashing givens can reach it).
+ * d_puzzles and d_solutions may alias.
  * `ordered` != 0 selects frontier mode: once board i is solved, boards j > i
  * are abandoned (status SDK_CANCELLED) and the lowest solved index is kept in
  * the workspace (sdk_read_stats out[4]). */
@@ -94,18 +99,12 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 /* Solve-kernel selection (library extension, no reference counterpart):
  * SDK_KERNEL_AUTO (default) SDK_KERNEL_PLANE for batches of 8192 boards or
  * more, SDK_KERNEL_PACKED below; SDK_KERNEL_PLANE one lane per board on
- * digit-plane bitboards
- * (boards with clashing givens or very deep searches go to a second,
- * wave-per-board pass); SDK_KERNEL_PACKED one wavefront per board, both cells
- * of a lane packed in one word; SDK_KERNEL_WAVE one wavefront per board, one register
- * set per cell; SDK_KERNEL_PAIR two boards per wavefront; SDK_KERNEL_LANE one
- * lane per board, nibble cells.  All give the same results.  0 restores the
- * default (or $SDK_SOLVE_KERNEL = auto|plane|p|2|3|l).
+ * digit-plane bitboards (boards with clashing givens or very deep searches
+ * go to a wave-per-board pass); SDK_KERNEL_PACKED one wavefront per board,
+ * both cells of a lane packed in one word.  Both give the same results.
+ * 0 restores the default (or $SDK_SOLVE_KERNEL = auto|plane|packed).
  * Returns the previous selection, -1 for an unknown value. */
 #define SDK_KERNEL_AUTO 1
-#define SDK_KERNEL_WAVE 2
-#define SDK_KERNEL_PAIR 3
-#define SDK_KERNEL_LANE 4
 #define SDK_KERNEL_PACKED 5
 #define SDK_KERNEL_PLANE 6
 int sdk_set_solve_kernel(int kernel);

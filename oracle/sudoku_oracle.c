@@ -200,6 +200,15 @@ void oracle_solve_batch_rowmajor(const uint8_t *in, uint8_t *out, int32_t *statu
     }
 }
 
+/* Batch form of oracle_solve_node (node.py:62-74 with is_valid_move). */
+void oracle_solve_batch_node(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n)
+{
+    for (int64_t p = 0; p < n; p++) {
+        memcpy(out + p * 81, in + p * 81, 81);
+        status[p] = oracle_solve_node(out + p * 81);
+    }
+}
+
 /* Test helper: number of completions (up to `limit`) under the reference's
  * constraint (every empty cell differs from its filled peers). */
 static int count_rec(uint8_t *g, int limit, int *count)

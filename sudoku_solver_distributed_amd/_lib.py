@@ -34,9 +34,9 @@ EXPORTS = (
     "sdk_device_cu_count",
     "sdk_set_solve_kernel",
 )
-SDK_KERNELS = {"auto": 1, "wave": 2, "pair": 3, "lane": 4, "packed": 5, "plane": 6}
+SDK_KERNELS = {"auto": 1, "packed": 5, "plane": 6}
 # device symbol of each solve kernel (rocprofv3 Kernel_Name, profiles/pmc_<symbol>.json)
-KERNEL_SYMBOLS = {1: "plane_kernel", 2: "solve_kernel", 3: "solve2_kernel", 4: "lane_kernel", 5: "solvep_kernel", 6: "plane_kernel"}
+KERNEL_SYMBOLS = {1: "plane_kernel", 5: "solvep_kernel", 6: "plane_kernel"}
 
 _lib = None
 

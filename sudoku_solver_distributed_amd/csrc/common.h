@@ -1,6 +1,6 @@
-// common.h -- definitions shared by the solve kernels' translation units
-// (sudoku_kernels.hip: wave-per-board kernels + C ABI; plane_kernels.hip: the
-// lane-per-board digit-plane kernel, built with its own scheduler options).
+// common.h -- definitions shared by the two translation units
+// (sudoku_kernels.hip: wave-per-board kernel, check / task / frontier kernels
+// and the C ABI; plane_kernels.hip: the lane-per-board digit-plane kernel).
 #ifndef SDK_COMMON_H
 #define SDK_COMMON_H
 
@@ -30,14 +30,6 @@ enum {
     WS_WORDS = 16
 };
 
-struct __attribute__((aligned(16))) WaveLds {
-    uint32_t M[28];  // unit masks of filled cells (rows 0-8, columns 9-17, boxes 18-26)
-    uint32_t T[28];  // per unit: digits that are candidates of >= 2 of its empty cells
-    uint32_t C[128]; // per cell: candidate mask published for the unit gather (0 = filled; 81.. padding)
-    uint32_t bad;    // units whose GIVENS repeat a digit (hidden-single rules off there)
-    uint32_t pad[3];
-};
-
 __device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
 
 // Orders this wave's LDS accesses (a single wave's DS ops execute in order;
@@ -47,24 +39,6 @@ __device__ __forceinline__ void wave_lds_sync()
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
     __builtin_amdgcn_wave_barrier();
-}
-
-// Order this wave's LDS accesses for the compiler only.  A wavefront's DS
-// instructions execute in issue order, so a lane's read issued after another
-// lane's write/atomic of the same word sees it without waiting for the
-// write's return: the sweep's round trips (atomics -> mask reads, publish ->
-// gather -> T reads) overlap in the LDS pipeline instead of each draining
-// lgkmcnt.  The signal fence keeps the compiler from moving accesses across.
-#ifndef SDK_LDS_INORDER
-#define SDK_LDS_INORDER 0
-#endif
-__device__ __forceinline__ void wave_lds_order()
-{
-#if SDK_LDS_INORDER
-    __atomic_signal_fence(__ATOMIC_SEQ_CST);
-#else
-    wave_lds_sync();
-#endif
 }
 
 // wave-uniform "any lane": the ballot's SGPR pair, no VGPR round trip

@@ -1,11 +1,12 @@
-// packed_solver.h -- v4 solve kernel: one board per wavefront, both cells of
-// a lane packed into one 32-bit word (included by sudoku_kernels.hip after
-// the v2 kernel; shares its workspace layout, walk orders and queue).
+// packed_solver.h -- wave-per-board solve kernel: one board per wavefront,
+// both cells of a lane packed into one 32-bit word (included by
+// sudoku_kernels.hip; shares its workspace layout, walk orders and queue).
 //
-// Same contract and the same propagation rules as v2 (naked singles; hidden
-// singles when no naked single is left; clash and empty-unit detection;
-// branching on the walk's next cell, digits ascending), so the same first
-// completion.  What changes is the arithmetic:
+// Propagation rules: naked singles; hidden singles when no naked single is
+// left; clash and empty-unit detection; branching on the walk's next cell,
+// digits ascending -- so the walk's first completion.
+// Node order additionally reproduces node.py's is_valid_move short-circuit
+// (node.py:44-45) exactly: see "literal mode" below.  The arithmetic:
 //   * lane l owns cell l in the low half and, for l < 17, cell 64+l in the
 //     high half of every per-lane word.  Lanes >= 17 carry a phantom high
 //     cell that is always filled and whose units are the dummy word 27;
@@ -22,6 +23,8 @@
 //     new placements) instead of v2's eleven per-slot registers.
 #ifndef SDK_PACKED_SOLVER_H
 #define SDK_PACKED_SOLVER_H
+
+enum { PROP_OPEN = 0, PROP_DEAD = 1, PROP_SOLVED = 2 };
 
 typedef unsigned short sdk_u16x2 __attribute__((ext_vector_type(2)));
 typedef short sdk_i16x2 __attribute__((ext_vector_type(2)));
@@ -63,7 +66,9 @@ struct PCells {
     uint32_t D;   // one-hot digit per half (0 = empty)
     uint32_t EK;  // PK_EMPTY per empty half, 0 per filled (or phantom) half
     uint32_t LV;  // depth at which each half was filled (givens / phantom: 0)
-    uint32_t G;   // one-hot given per half
+    uint32_t G;   // one-hot given per half (the input board: written back on failure)
+    uint32_t GS;  // one-hot "given" of the current propagation root (= G except below a
+                  // literal-mode node, where every cell filled there counts as given)
     uint32_t NW;  // one-hot placements since the last sweep (not yet in the unit masks)
     int u0, u1, u2, u3, u4, u5;  // units (rows 0-8, columns 9-17, boxes 18-26) of the low / high cell
     int ub, us1, us2;            // unit gather (lanes < 27): cells ub + k*us1 + (k/3)*us2
@@ -98,20 +103,21 @@ __device__ __forceinline__ bool pload_board(const uint8_t *__restrict__ src, int
     b = lane < 17 ? (uint32_t)src[64 + lane] : 0u;
     s.D = onehot(a) | (onehot(b) << 16);
     s.G = s.D;
+    s.GS = s.D;
     s.EK = (a == 0 ? PK_EMPTY : 0u) | ((lane < 17 && b == 0) ? (PK_EMPTY << 16) : 0u);
     s.LV = 0;
     s.NW = 0;
     return !wany(a > 9 || b > 9);
 }
 
-// Givens' unit masks (both halves; returned in lanes 0..26, W.M holds them)
-// and the bad-unit mask.
+// Root givens' (s.GS) unit masks (both halves; returned in lanes 0..26, W.M
+// holds them) and the bad-unit mask.
 __device__ __forceinline__ uint32_t pbuild_given_masks(PackLds &W, int lane, const PCells &s, uint32_t &bad)
 {
     if (lane < 28) W.M[lane] = 0;
     if (lane == 0) W.bad = 0;
     wave_lds_sync();
-    const uint32_t g0 = s.G & 0xFFFFu, g1 = s.G >> 16;
+    const uint32_t g0 = s.GS & 0xFFFFu, g1 = s.GS >> 16;
     uint32_t d = 0;
     if (g0) {
         const uint32_t bd = g0 | (g0 << 16);
@@ -141,7 +147,7 @@ __device__ __forceinline__ int psweep(PackLds &W, int lane, PCells &s, uint32_t 
     uint32_t f;
     if (rebuild) {
         if (lane < 27) W.M[lane] = gmask;
-        f = s.D & ~s.G;
+        f = s.D & ~s.GS;
     } else {
         f = s.NW;
     }
@@ -255,48 +261,161 @@ __device__ __forceinline__ void pstore_board(uint8_t *__restrict__ dst, int lane
     if (lane < 17) dst[64 + lane] = (uint8_t)digit_of(x >> 16);
 }
 
-// Full search of one board (v2's search() on packed cells).
+// ------------------------------------------------------------ literal mode
+// node.py's walk tests a digit with is_valid_move (node.py:42-60), which
+// answers True whenever every row, column and box already sums to 45
+// (node.py:44-45, SudokuSolver.check).  With an empty cell on the board that
+// needs repeated digits, so only boards whose givens clash can get there --
+// and then the walk may put ANY digit in the cell.  Propagation (naked /
+// hidden singles, dead-cell tests) presumes the plain rule below such a
+// node, so in node order the search runs "literally" (no propagation, branch
+// on the first empty cell, candidates = the digits is_valid_move accepts)
+// while such a node is still reachable:
+//
+//   R(N) = every unit u has  s_u <= 45 <= s_u + 9 e_u  (sum / empty cells)
+//          and some empty cell has a repeated digit in its row, its column
+//          AND its box.
+//
+// Along a path s_u only grows, s_u + 9 e_u only shrinks, and plain moves
+// create no repeated digit, so R is monotone: once R(N) is false the whole
+// subtree is the plain walk, rooted at N (every cell filled at N counts as a
+// given there: GS).  A node where the short-circuit fires has R true (its
+// cell's units sum to 45 with a hole, so they repeat a digit).
+struct LitEval {
+    bool R;        // a short-circuit node is reachable below (and at) this node
+    bool s45;      // every unit sums to 45 here: is_valid_move accepts 1..9
+    uint32_t cand; // lane: candidates of its low (bits 0-8) / high (16-24) cell
+};
+
+__device__ __forceinline__ LitEval lit_eval(PackLds &W, int lane, const PCells &s)
+{
+    // T[u]: sum | filled count << 8; C[u]: digits present; pad[0]: units
+    // with a repeated digit.  (T and C are psweep phase-B scratch.)
+    if (lane < 28) { W.T[lane] = 0; W.C[lane] = 0; }
+    if (lane == 0) W.pad[0] = 0;
+    wave_lds_sync();
+    const uint32_t dlo = digit_of(s.D & 0xFFFFu), dhi = digit_of(s.D >> 16);
+    uint32_t dup = 0;
+    if (dlo) {
+        const uint32_t add = dlo | (1u << 8), bit = 1u << (dlo - 1);
+        atomicAdd(&W.T[s.u0], add); atomicAdd(&W.T[s.u1], add); atomicAdd(&W.T[s.u2], add);
+        if (atomicOr(&W.C[s.u0], bit) & bit) dup |= 1u << s.u0;
+        if (atomicOr(&W.C[s.u1], bit) & bit) dup |= 1u << s.u1;
+        if (atomicOr(&W.C[s.u2], bit) & bit) dup |= 1u << s.u2;
+    }
+    if (dhi) {  // phantom halves (lanes >= 17) hold no digit
+        const uint32_t add = dhi | (1u << 8), bit = 1u << (dhi - 1);
+        atomicAdd(&W.T[s.u3], add); atomicAdd(&W.T[s.u4], add); atomicAdd(&W.T[s.u5], add);
+        if (atomicOr(&W.C[s.u3], bit) & bit) dup |= 1u << s.u3;
+        if (atomicOr(&W.C[s.u4], bit) & bit) dup |= 1u << s.u4;
+        if (atomicOr(&W.C[s.u5], bit) & bit) dup |= 1u << s.u5;
+    }
+    if (dup) atomicOr(&W.pad[0], dup);
+    wave_lds_sync();
+    const uint32_t dups = __builtin_amdgcn_readfirstlane(W.pad[0]);
+    bool unit_ok = true, is45 = true;
+    if (lane < 27) {
+        const uint32_t t = W.T[lane], sum = t & 0xFFu, empty = 9u - (t >> 8);
+        unit_ok = sum <= 45u && sum + 9u * empty >= 45u;
+        is45 = sum == 45u;
+    }
+    const bool clo = (s.EK & 0x8000u) && ((dups >> s.u0) & (dups >> s.u1) & (dups >> s.u2) & 1u);
+    const bool chi = (s.EK & 0x80000000u) && ((dups >> s.u3) & (dups >> s.u4) & (dups >> s.u5) & 1u);
+    LitEval r;
+    r.R = !wany(!unit_ok) && wany(clo || chi);
+    r.s45 = !wany(!is45);
+    const uint32_t ulo = W.C[s.u0] | W.C[s.u1] | W.C[s.u2], uhi = W.C[s.u3] | W.C[s.u4] | W.C[s.u5];
+    r.cand = (~ulo & 0x1FFu) | ((~uhi & 0x1FFu) << 16);
+    return r;
+}
+
+// Full search of one board.
 __device__ __forceinline__ int psearch(PackLds &W, int lane, PCells &s, int64_t idx, int order, const int64_t *best,
                                        uint32_t &guesses, uint32_t &sweeps)
 {
     uint32_t bad;
-    const uint32_t gmask = pbuild_given_masks(W, lane, s, bad);
+    uint32_t gmask = pbuild_given_masks(W, lane, s, bad);
+    // literal mode is possible only in node order, with repeated givens
+    bool lit = order == SDK_ORDER_NODE && bad != 0;
+    uint32_t lit_top = 0;  // literal mode: depth at which the plain walk took over
     bool rebuild = false;  // W.M already holds exactly the givens
     uint32_t depth = 0;
     uint32_t stk0 = 0, stk1 = 0;  // DFS stack: level k lives in lane k&63 of stk(k>>6)
     uint32_t c9;
+    bool in_lit = lit;
+    int result;
     for (;;) {
-        const int st = ppropagate(W, lane, s, gmask, bad, depth, rebuild, c9, sweeps);
-        if (st == PROP_SOLVED) return SDK_SOLVED;
-        if (st == PROP_OPEN) {
-            // branch on the walk's next cell, smallest digit first
-            const uint64_t eb0 = __builtin_amdgcn_ballot_w64((s.EK & 0x8000u) != 0);
-            const uint64_t eb1 = __builtin_amdgcn_ballot_w64((s.EK & 0x80000000u) != 0);
-            const int cell = order_cell(eb0, eb1, order);
-            const uint32_t cand = cell < 64 ? rdlane(c9, cell) & 0x1FFu : rdlane(c9, cell - 64) >> 16;
-            if (cand == 0) return SDK_FAULT;  // unreachable: a fixpoint has no empty cell without candidates
-            const uint32_t d = lowbit(cand);
-            const uint32_t entry = ((uint32_t)cell << 9) | (cand ^ d);
-            if (depth < 64) { if (lane == (int)depth) stk0 = entry; }
-            else if (lane == (int)depth - 64) stk1 = entry;
-            depth++;
-            pplace(s, lane, cell, d, depth);
-            guesses++;
-            if (best && (guesses & 63u) == 0) {
-                const int64_t b = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if (__builtin_amdgcn_readfirstlane((int)(b < idx))) return SDK_CANCELLED;
+        bool dead = false;
+        if (in_lit) {
+            const LitEval e = lit_eval(W, lane, s);
+            if (e.R) {
+                // node.py:63-72 literally: first empty cell, digits is_valid_move accepts
+                const uint64_t eb0 = __builtin_amdgcn_ballot_w64((s.EK & 0x8000u) != 0);
+                const uint64_t eb1 = __builtin_amdgcn_ballot_w64((s.EK & 0x80000000u) != 0);
+                const int cell = order_cell(eb0, eb1, SDK_ORDER_NODE);  // R => an empty cell exists
+                const uint32_t cand = e.s45 ? 0x1FFu
+                                    : cell < 64 ? rdlane(e.cand, cell) & 0x1FFu : rdlane(e.cand, cell - 64) >> 16;
+                if (cand == 0) {
+                    dead = true;
+                } else {
+                    const uint32_t d = lowbit(cand);
+                    const uint32_t entry = ((uint32_t)cell << 9) | (cand ^ d);
+                    if (depth < 64) { if (lane == (int)depth) stk0 = entry; }
+                    else if (lane == (int)depth - 64) stk1 = entry;
+                    depth++;
+                    pplace(s, lane, cell, d, depth);
+                    guesses++;
+                    continue;
+                }
+            } else {
+                // the plain walk from here: every filled cell is a given below
+                in_lit = false;
+                lit_top = depth;
+                s.GS = s.D;
+                s.NW = 0;
+                gmask = pbuild_given_masks(W, lane, s, bad);
+                rebuild = false;
             }
-            continue;
+        }
+        if (!dead) {
+            const int st = ppropagate(W, lane, s, gmask, bad, depth, rebuild, c9, sweeps);
+            if (st == PROP_SOLVED) { result = SDK_SOLVED; break; }
+            if (st == PROP_OPEN) {
+                // branch on the walk's next cell, smallest digit first
+                const uint64_t eb0 = __builtin_amdgcn_ballot_w64((s.EK & 0x8000u) != 0);
+                const uint64_t eb1 = __builtin_amdgcn_ballot_w64((s.EK & 0x80000000u) != 0);
+                const int cell = order_cell(eb0, eb1, order);
+                const uint32_t cand = cell < 64 ? rdlane(c9, cell) & 0x1FFu : rdlane(c9, cell - 64) >> 16;
+                if (cand == 0) { result = SDK_FAULT; break; }  // unreachable: a fixpoint has no empty cell without candidates
+                const uint32_t d = lowbit(cand);
+                const uint32_t entry = ((uint32_t)cell << 9) | (cand ^ d);
+                if (depth < 64) { if (lane == (int)depth) stk0 = entry; }
+                else if (lane == (int)depth - 64) stk1 = entry;
+                depth++;
+                pplace(s, lane, cell, d, depth);
+                guesses++;
+                if (best && (guesses & 63u) == 0) {
+                    const int64_t b = __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (__builtin_amdgcn_readfirstlane((int)(b < idx))) { result = SDK_CANCELLED; break; }
+                }
+                continue;
+            }
         }
         // dead: backtrack to the deepest level with an untried digit
         rebuild = true;
         s.NW = 0;
+        bool exhausted = false;
         for (;;) {
-            if (depth == 0) return SDK_UNSOLVABLE;
+            if (depth == 0) { exhausted = true; break; }
             const uint32_t top = depth - 1;
             const uint32_t entry = top < 64 ? rdlane(stk0, top) : rdlane(stk1, top - 64);
             pundo(s, depth);
             depth = top;
+            if (lit && !in_lit && top < lit_top) {
+                // back above the node where the plain walk took over: literal again
+                in_lit = true;
+                s.GS = s.G;
+            }
             const uint32_t rem = entry & 0x1FFu;
             if (rem == 0) continue;
             const int cell = (int)(entry >> 9);
@@ -309,7 +428,10 @@ __device__ __forceinline__ int psearch(PackLds &W, int lane, PCells &s, int64_t 
             guesses++;
             break;
         }
+        if (exhausted) { result = SDK_UNSOLVABLE; break; }
     }
+    s.GS = s.G;
+    return result;
 }
 
 // One board (index p) by the whole wave: load, search, store, status.

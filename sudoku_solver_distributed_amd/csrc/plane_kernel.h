@@ -116,8 +116,13 @@ __device__ __forceinline__ unsigned long long rdlane64(unsigned long long v, int
     return ((unsigned long long)rdlane((uint32_t)(v >> 32), l) << 32) | rdlane((uint32_t)v, l);
 }
 
-// number of lanes executing this point (the exec mask of a divergent branch)
-__device__ __forceinline__ uint32_t lanes_here() { return (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(true)); }
+// sum of a per-lane counter over the wave (all lanes active)
+__device__ __forceinline__ uint32_t wave_sum(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o);
+    return v;
+}
 
 #ifndef SDK_PLANE_WAVES_PER_EU
 #define SDK_PLANE_WAVES_PER_EU 4
@@ -139,7 +144,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     int64_t p = -1;       // this lane's board
     int state = PL_IDLE;
     uint32_t depth = 0;
-    // wave-uniform statistics
+    // per-lane statistics (each lane counts its own boards' events; summed
+    // over the wave at exit)
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     bool drained = false;  // the queue is empty
 
@@ -154,7 +160,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         drained = (int64_t)base + 64 >= n;
         const int64_t q = (int64_t)base + lane;
         if (q < n) {
-            fin += lanes_here();
+            fin++;
             const uint8_t *src = puzzles + q * 81;
             uint32_t x[21];
 #pragma unroll
@@ -184,7 +190,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
             // ---- store finished boards, one at a time over the whole wave
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
-            solved += (uint32_t)__builtin_popcountll(m);
+            solved += state == PL_SOLVED;
             while (m) {
                 const int i = __builtin_ctzll(m);
                 m &= m - 1;
@@ -226,8 +232,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     // SOLVED result needs every unit to hold every digit, so
                     // such givens never reach the store above.)
                     if (lane == 0) status[pi] = SDK_DEFERRED;
-                    fin--;
-                    deferred++;
+                    if (lane == i) { fin--; deferred++; }
                     continue;
                 }
                 plane_copy_board(puzzles + pi * 81, sols + pi * 81, lane);
@@ -252,7 +257,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 for (int64_t q = (int64_t)base; m && q < n; ++q) {
                     const int i = __builtin_ctzll(m);
                     m &= m - 1;
-                    fin++;
+                    if (lane == i) fin++;
                     const uint8_t *src = puzzles + q * 81;
                     // slots holding no cell read the sentinel 0x100 (no byte value)
                     const uint32_t a0 = c0 >= 0 ? src[c0] : 0x100u, a1 = c1 >= 0 ? src[c1] : 0x100u;
@@ -295,9 +300,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 if (loaded) {
                     if (plane::givens_clash(B, given)) {
                         status[p] = SDK_DEFERRED;
-                        const uint32_t k = lanes_here();
-                        fin -= k;
-                        deferred += k;
+                        fin--;
+                        deferred++;
                     } else {
                         state = PL_ACTIVE;
                     }
@@ -309,7 +313,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         if (state != PL_ACTIVE) continue;
 
         // ---- one pass of this lane's board
-        passes += lanes_here();
+        passes++;
         uint32_t und[3];
         const int r = plane::pass(B, und);
         if (r == plane::SOLVED) {
@@ -319,9 +323,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         } else if (r == plane::STUCK) {
             if (depth == PLANE_MAX_DEPTH) {
                 status[p] = SDK_DEFERRED;  // too deep for the stack: the packed kernel's
-                const uint32_t k = lanes_here();
-                fin -= k;
-                deferred += k;
+                fin--;
+                deferred++;
                 state = PL_IDLE;
             } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
                 state = PL_CANCELLED;
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 for (int w = 0; w < 27; ++w) stk.put(depth, w, B.P[w / 3][w % 3]);
                 stk.put(depth, plane::STACK_ENTRY, plane::make_entry(band, pos, cand ^ d));
                 depth++;
-                guesses += lanes_here();
+                guesses++;
                 plane::set_cell(B, band, pos, d);
             }
         } else if (r == plane::DEAD) {
@@ -354,15 +357,20 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 B.Det[0] = B.Det[1] = B.Det[2] = 0;
                 stk.put(depth, plane::STACK_ENTRY, e & ~(d << 8));
                 depth++;
-                guesses += lanes_here();
+                guesses++;
                 plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
                 break;
             }
         }
     }
-    // per-wave statistics: one atomic per counter and wave
+    // per-wave statistics: the lanes' counts summed, one atomic per counter and wave
+    fin = wave_sum(fin);
+    solved = wave_sum(solved);
+    guesses = wave_sum(guesses);
+    passes = wave_sum(passes);
+    deferred = wave_sum(deferred);
     if (lane == 0 && deferred) atomicAdd(&ws[WS_DEFERRED], (unsigned long long)deferred);
-    if (lane == 0 && fin) {
+    if (lane == 0 && (fin | deferred)) {
         atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
         atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
         atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);

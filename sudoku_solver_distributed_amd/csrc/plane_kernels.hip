@@ -1,9 +1,8 @@
 // plane_kernels.hip -- translation unit of the lane-per-board digit-plane
-// solve kernel (plane_kernel.h).  Built on its own (build.py) with
-// -mllvm -amdgpu-sched-strategy=iterative-minreg: the default scheduler
-// interleaves the nine digits of a pass for ILP and needs ~136 VGPRs, the
-// min-register strategy ~103, so four waves fit per SIMD without spills
-// (one wave alone issues VALU every 4 cycles, two saturate the SIMD).
+// solve kernel (plane_kernel.h), built on its own by build.py (LLVM's default
+// machine scheduler; $SDK_PLANE_SCHED selects another strategy for A/B
+// builds).  The pass pins its board between digits (plane_solver.h PS_PIN),
+// which keeps it at ~113 VGPRs: four waves per SIMD, no spills.
 #include "common.h"
 #include "plane_kernel.h"
 

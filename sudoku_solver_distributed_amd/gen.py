@@ -25,9 +25,13 @@ import torch
 from .solver import SDK_SOLVED, as_boards, get_solver
 from .sudoku import Sudoku
 
-# 17-clue boards with exactly one solution (certified by tests/test_workloads.py
-# with the oracle's counter); the last one is the "brute-force resistant" board
-# whose solution's first row is 987654321 -- a worst case for the walk.
+# 17-clue boards with exactly one solution (certified by
+# tests/test_oracle.py::test_seeds_unique with the oracle's counter); the last
+# one is the "brute-force resistant" board whose solution's first row is
+# 987654321 -- a worst case for the walk.  hard17_batch makes every benchmark
+# board from these six, so the set has six isomorphism classes; their
+# logical difficulty is mostly singles (0.5 guesses per board), which is why
+# bench.py also reports a search-heavy side set (hard_search_batch).
 SEEDS_17 = (
     "000000010400000000020000000000050407008000300001090000300400200050100000000806000",
     "000000010400000000020000000000050604008000300001090000300400200050100000000807000",

@@ -35,13 +35,14 @@ def _require_gpu(device) -> torch.device:
     return dev
 
 
-def as_boards(x, device=None) -> torch.Tensor:
+def as_boards(x, device=None, max_value: int = 9) -> torch.Tensor:
     """Anything board-like -> contiguous (n, 81) uint8 tensor (host or device).
 
     Accepts a 9x9 list of lists (the reference's board type), a list of such
     boards, an 81-char string, numpy arrays and tensors.  Raises ValueError on
-    a cell outside 0..9 (the reference would silently compare such values;
-    this boundary rejects them up front)."""
+    a cell outside 0..max_value: solving takes 0..9 (the reference's walk
+    would silently compare other values), the check kernels take any byte
+    (0..255, the reference's sum / set arithmetic on them)."""
     if isinstance(x, str):
         x = [int(c) for c in x]
     if isinstance(x, torch.Tensor):
@@ -50,15 +51,15 @@ def as_boards(x, device=None) -> torch.Tensor:
         a = np.asarray(x)
         if a.dtype == object:
             raise ValueError("ragged board")
-        if a.size and (a.min() < 0 or a.max() > 9):
-            raise ValueError("board cells must be integers 0..9")
+        if a.size and (a.min() < 0 or a.max() > max_value):
+            raise ValueError(f"board cells must be integers 0..{max_value}")
         t = torch.from_numpy(np.ascontiguousarray(a.astype(np.uint8)))
     if t.numel() % 81 != 0:
         raise ValueError(f"board data of {t.numel()} cells is not a multiple of 81")
     t = t.reshape(-1, 81)
     if t.dtype != torch.uint8:
-        if t.numel() and (int(t.min()) < 0 or int(t.max()) > 9):
-            raise ValueError("board cells must be integers 0..9")
+        if t.numel() and (int(t.min()) < 0 or int(t.max()) > max_value):
+            raise ValueError(f"board cells must be integers 0..{max_value}")
         t = t.to(torch.uint8)
     if device is not None:
         t = t.to(device, non_blocking=True)
@@ -110,7 +111,7 @@ class BatchSolver:
 
     def check(self, grids, mode: int = 0, stream=None) -> torch.Tensor:
         """mode 0: Sudoku.check (sudoku.py:119-140); mode 1: node.py:82-116."""
-        g = self._dev(as_boards(grids))
+        g = self._dev(as_boards(grids, max_value=255))
         ok = torch.empty(g.shape[0], dtype=torch.int32, device=self.device)
         with torch.cuda.device(self.device):
             rc = self.lib.sdk_check_batch(g.data_ptr(), ok.data_ptr(), g.shape[0], mode, self._stream(stream))
@@ -119,7 +120,7 @@ class BatchSolver:
 
     def first_candidate(self, grids, cells, stream=None) -> torch.Tensor:
         """node.py:76-80 per (board, cell) task; 0 means None."""
-        g = self._dev(as_boards(grids))
+        g = self._dev(as_boards(grids, max_value=255))
         c = self._dev(torch.as_tensor(cells, dtype=torch.int32).reshape(-1))
         if c.shape[0] != g.shape[0]:
             raise ValueError("one cell index per board")

@@ -99,15 +99,31 @@ class Sudoku:
     # sudoku.py:119-140 -- whole-board verdict on the GPU.  The reference
     # charges _limit_calls once per unit it inspects (rows, columns, squares,
     # stopping at the first bad one); with a non-zero delay we charge the same.
+    # Any byte value goes to the kernel (it does the reference's sum / set
+    # arithmetic on bytes); a cell that is not a byte at all (negative, > 255,
+    # not an int) cannot be a GPU operand, and the reference's own unit
+    # helpers give the verdict -- a False unless that unit arithmetic says so,
+    # never an exception (sudoku.py:85 returns False).
     def check(self, base_delay=None, interval=None, threshold=None):
+        if not self._byte_grid():
+            return self._units_until_failure() == 28
         ok = bool(Sudoku.check_many([self.grid])[0].item())
         delay = self.base_delay if base_delay is None else base_delay
         if delay:
-            for _ in range(27 if ok else self._units_until_failure()):
+            for _ in range(min(27, self._units_until_failure())):
                 self._limit_calls(base_delay, interval, threshold)
         return ok
 
+    def _byte_grid(self) -> bool:
+        try:
+            return len(self.grid) == 9 and all(
+                len(r) == 9 and all(type(v) is int and 0 <= v <= 255 for v in r) for r in self.grid)
+        except TypeError:
+            return False
+
     def _units_until_failure(self) -> int:
+        """1-based index of the first unit (rows, columns, squares) failing
+        sudoku.py:85's test, 28 if none does."""
         g = self.grid
         units = [g[r] for r in range(9)]
         units += [[g[r][c] for r in range(9)] for c in range(9)]
@@ -116,7 +132,7 @@ class Sudoku:
         for k, u in enumerate(units):
             if sum(u) != 45 or len(set(u)) != 9:
                 return k + 1
-        return 27
+        return 28
 
     # ----------------------------------------------------------- GPU batch
     def solve(self) -> bool:

@@ -3,7 +3,7 @@
 Run only in the build container (the reference is mounted read-only at
 /root/reference there; it does not exist on the GPU box):
 
-    python tests/golden/make_golden.py [/root/reference] [--gen] [--solve] [--check] [--node]
+    python tests/golden/make_golden.py [/root/reference] [--gen] [--solve] [--check] [--node] [--sc] [--peer]
 
 It imports the reference's gen.py, sudoku.py and node.py and records
 inputs + outputs as JSON data (no reference source is copied):
@@ -19,6 +19,21 @@ inputs + outputs as JSON data (no reference source is copied):
 * golden_node.json    -- node.SudokuSolver.solve_sudoku_destributed
                          (node.py:76-80) tasks and solve_sudoku_recursive
                          (node.py:62-74) on small boards
+* golden_sc.json      -- node.SudokuSolver.solve_sudoku (node.py:31-40, 62-74)
+                         on boards where is_valid_move's short-circuit
+                         (node.py:44-45: every unit sums to 45) can fire:
+                         a full grid with one cell emptied and three cells
+                         shifted so every unit still sums to 45, plus 0-5
+                         extra blanks.  `sc_fires` marks the boards whose
+                         answer differs from a walk without the short-circuit
+                         (the build container's oracle decides; the expected
+                         output is the reference's).
+* golden_peer.json    -- node.P2PNode.peer_sudoku_solve (node.py:534-557), the
+                         reference's HTTP /solve path, on a fresh single node
+                         with handicap 0 (no peers: every cell task runs
+                         locally, node.py:443-449): README puzzle + gen boards.
+                         Its answer can be partial or invalid; a 5 s alarm
+                         records the boards on which it never returns.
 """
 from __future__ import annotations
 
@@ -48,6 +63,10 @@ def s81(board):
 
 def b81(s):
     return [[int(s[r * 9 + c]) for c in range(9)] for r in range(9)]
+
+
+def b81s(s):
+    return [int(x) for x in s]
 
 
 def run_limited(fn, seconds):
@@ -81,6 +100,25 @@ _FULL = NAMED["full_valid"]
 NAMED["clash_completable"] = ("88" + _FULL[2:30] + "0" + _FULL[31:50] + "0" + _FULL[51:70] + "0"
                               + _FULL[71:])
 assert all(len(v) == 81 for v in NAMED.values())
+
+def _sc_board(full, rng, extra):
+    """Empty cell A=(r,c) (value v), add v to B=(r,c2) and C=(r3,c), subtract
+    v from D=(r3,c2), c2 in A's box column: every unit still sums to 45."""
+    g = [int(x) for x in full]
+    for _ in range(1000):
+        r, c = rng.randrange(9), rng.randrange(9)
+        c2, r3 = 3 * (c // 3) + rng.randrange(3), rng.randrange(9)
+        if c2 == c or r3 == r:
+            continue
+        A, B, C, D = r * 9 + c, r * 9 + c2, r3 * 9 + c, r3 * 9 + c2
+        v = g[A]
+        if g[B] + v <= 9 and g[C] + v <= 9 and g[D] - v >= 0:
+            g[A], g[B], g[C], g[D] = 0, g[B] + v, g[C] + v, g[D] - v
+            for e in rng.sample([i for i in range(81) if g[i]], extra):
+                g[e] = 0
+            return "".join(map(str, g))
+    return None
+
 
 def main(ref_dir, stages):
     sys.path.insert(0, ref_dir)
@@ -205,10 +243,60 @@ def main(ref_dir, stages):
                  "solution": s81(board), "solved_puzzles": s.solved_puzzles})
         with open(os.path.join(HERE, "golden_node.json"), "w") as f:
             json.dump(node_cases, f, indent=0)
+    # ------------------------------------------------------ short-circuit
+    if "sc" in stages:
+        sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+        import numpy as np
+        from oracle import oracle as O  # filter only: which boards the short-circuit changes
+        fulls = [c["solution"] for c in gen_cases if c["empty_boxes"] == 0]
+        rng = random.Random(2026)
+        sc_cases, fires = [], 0
+        while len(sc_cases) < 64:
+            p = _sc_board(fulls[len(sc_cases) % len(fulls)], rng, rng.choice([0, 0, 1, 2, 3, 5]))
+            if p is None:
+                continue
+            plain, pst = O.solve_batch(np.array([b81s(p)], dtype=np.uint8), order="node")
+            board = b81(p)
+            s_ = node.SudokuSolver(0)
+            try:
+                with contextlib.redirect_stdout(io.StringIO()):
+                    out = run_limited(lambda: s_.solve_sudoku(board), 30)
+            except _Timeout:
+                continue
+            sol = s81(board)
+            differs = (out is not None) != bool(pst[0]) or sol != "".join(map(str, plain[0].tolist()))
+            if not differs and fires * 2 < len(sc_cases):
+                continue  # keep at least half the fixture on boards where it fires
+            fires += differs
+            sc_cases.append({"puzzle": p, "solved": out is not None, "solution": sol, "sc_fires": differs})
+        with open(os.path.join(HERE, "golden_sc.json"), "w") as f:
+            json.dump(sc_cases, f, indent=0)
+        print("sc", len(sc_cases), "fires", fires)
+
+    # --------------------------------------------------------------- peer
+    if "peer" in stages:
+        boards = [("readme", NAMED["readme"])]
+        boards += [(f"gen{c['seed']}", c["puzzle"]) for c in gen_cases
+                   if c["empty_boxes"] in (5, 20, 40) and c["seed"] // 1000 < 6]
+        peer_cases = []
+        for name, p in boards:
+            with contextlib.redirect_stdout(io.StringIO()):
+                n = node.P2PNode("127.0.0.1", 0, handicap=0)
+                try:
+                    out = run_limited(lambda: n.peer_sudoku_solve(b81(p)), 5)
+                    res = s81(out) if out else None
+                except _Timeout:
+                    res = "TIMEOUT"
+            peer_cases.append({"name": name, "puzzle": p, "returned": res,
+                               "validations": n.solver.validations,
+                               "solved_puzzles": n.solver.solved_puzzles})
+        with open(os.path.join(HERE, "golden_peer.json"), "w") as f:
+            json.dump(peer_cases, f, indent=0)
+        print("peer", len(peer_cases))
     print("done", stages)
 
 
 if __name__ == "__main__":
     args = [a for a in sys.argv[1:] if not a.startswith("--")]
-    st = [a[2:] for a in sys.argv[1:] if a.startswith("--")] or ["gen", "solve", "check", "node"]
+    st = [a[2:] for a in sys.argv[1:] if a.startswith("--")] or ["gen", "solve", "check", "node", "sc", "peer"]
     main(args[0] if args else "/root/reference", set(st))

@@ -131,14 +131,15 @@ def test_invalid_bytes_rejected(solver):
     assert int(sols[1, 5]) == 12
 
 
-@pytest.mark.parametrize("kernel", ["auto", "plane"])
+@pytest.mark.parametrize("kernel", ["auto", "plane", "packed"])
 @pytest.mark.parametrize("order", ["gen", "node"])
 def test_duplicate_givens_vs_oracle(solver, order, kernel):
     """Clashing givens: the walk never tests givens, so such boards can still
     be completed (e.g. nearly full boards); compare where a completion exists
     and the board is otherwise unchanged-False.  `plane` forces the
     lane-per-board kernel, which tests for clashing givens only once a search
-    ends without a completion and then defers the board."""
+    ends without a completion and then defers the board.  Node order is
+    checked against the literal node.py walk (is_valid_move included)."""
     from sudoku_solver_distributed_amd import _lib
     prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
     try:
@@ -165,9 +166,43 @@ def _duplicate_givens_case(solver, order):
     assert (st[dead] == 0).all() and np.array_equal(sols[dead], base[dead])
     live = np.nonzero(~dead)[0]
     assert live.size > 100
-    want, wst = O.solve_batch(base[live], order=order)
+    want, wst = O.solve_batch(base[live], order="node_literal" if order == "node" else order)
     assert np.array_equal(st[live], wst)
     assert np.array_equal(sols[live], want)
+
+
+@pytest.mark.parametrize("kernel", ["auto", "plane", "packed"])
+def test_short_circuit_goldens(solver, kernel):
+    """node.py:44-45 (is_valid_move accepts any digit once every unit sums to
+    45): the reference's SudokuSolver.solve_sudoku outputs on boards where it
+    fires (tests/golden/golden_sc.json), in a small batch, and tiled into a
+    batch large enough for the plane kernel (auto) -- whose clash test hands
+    these boards to the wave kernel."""
+    from sudoku_solver_distributed_amd import _lib
+    cases = load_golden("golden_sc.json")
+    p = torch.tensor([b81(c["puzzle"]) for c in cases], dtype=torch.uint8)
+    want = [c["solution"] for c in cases]
+    prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
+    try:
+        for reps in (1, 160):  # 64 and 10240 boards
+            sols, st = solver.solve(p.repeat(reps, 1), order="node")
+            sols, st = sols.cpu().numpy(), st.cpu().numpy()
+            for k in range(len(cases) * reps):
+                c = cases[k % len(cases)]
+                assert (st[k] == 1) == c["solved"], (k, c["puzzle"])
+                assert _s(sols[k]) == want[k % len(cases)], (k, c["puzzle"])
+    finally:
+        solver.lib.sdk_set_solve_kernel(prev)
+
+
+def test_short_circuit_frontier(solver):
+    """Frontier split in node order on short-circuit boards: the lowest
+    solved frontier node is node.py's answer."""
+    for c in load_golden("golden_sc.json")[:16]:
+        ok, grid = solver.solve_one_split(torch.tensor([b81(c["puzzle"])], dtype=torch.uint8), target=64,
+                                          order="node")
+        assert ok == c["solved"], c["puzzle"]
+        assert _s(grid.cpu()) == c["solution"], c["puzzle"]
 
 
 def test_check_batch(solver):
@@ -247,6 +282,11 @@ def test_sudoku_class_api(solver):
     assert Sudoku(board).check() is True
     board[0][0], board[0][1] = board[0][1], board[0][0]
     assert Sudoku(board).check() is False
+    # sudoku.py:85 answers False (no exception) for cells outside 1..9
+    for bad in (10, 200, -3, 1000):
+        b2 = [r[:] for r in board]
+        b2[4][4] = bad
+        assert Sudoku(b2).check() is False
 
 
 def test_distributed_single_rank_gpu(solver):
@@ -266,7 +306,7 @@ def test_distributed_single_rank_gpu(solver):
     assert np.array_equal(sols.cpu().numpy(), w)
 
 
-@pytest.mark.parametrize("kernel", ["wave", "pair", "lane", "packed", "plane"])
+@pytest.mark.parametrize("kernel", ["packed", "plane"])
 def test_alternate_kernels_parity(solver, kernel):
     """The non-default solve kernels (sdk_set_solve_kernel): goldens, generated
     boards in both walks, clashing givens, invalid bytes, ordered mode and
@@ -308,3 +348,28 @@ def test_alternate_kernels_parity(solver, kernel):
         assert solver.stats()["best"] == 10
     finally:
         solver.lib.sdk_set_solve_kernel(prev)
+
+
+def test_stats_agree_between_kernels(solver):
+    """sdk_read_stats: every board counted once, and both solve kernels
+    branch on the same fixpoints, so the same number of guesses (the plane
+    kernel's per-lane counters are summed over the wave)."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    p = hard17_batch(20000, seed=3).to(solver.device)
+    got = {}
+    for kernel in ("packed", "plane"):
+        prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
+        try:
+            solver.stats(reset=True)
+            sols, st = solver.solve(p)
+            torch.cuda.synchronize()
+            got[kernel] = solver.stats(reset=True)
+            assert bool((st == 1).all())
+        finally:
+            solver.lib.sdk_set_solve_kernel(prev)
+    for k in ("packed", "plane"):
+        assert got[k]["finished"] == 20000 and got[k]["solved"] == 20000, got
+        assert got[k]["deferred"] == 0, got
+    assert got["plane"]["guesses"] == got["packed"]["guesses"], got
+    assert got["plane"]["sweeps"] > 20000 * 5, got
