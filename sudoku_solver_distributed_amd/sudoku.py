@@ -150,7 +150,7 @@ class Sudoku:
 
     @staticmethod
     def check_many(grids, mode: int = 0) -> torch.Tensor:
-        return get_solver().check(as_boards(grids), mode)
+        return get_solver().check(grids, mode)
 
     @staticmethod
     def solve_many(puzzles, ordered: bool = False):

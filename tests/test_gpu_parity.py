@@ -352,8 +352,11 @@ def test_alternate_kernels_parity(solver, kernel):
 
 def test_stats_agree_between_kernels(solver):
     """sdk_read_stats: every board counted once, and both solve kernels
-    branch on the same fixpoints, so the same number of guesses (the plane
-    kernel's per-lane counters are summed over the wave)."""
+    branch on the same fixpoints, so (nearly) the same number of guesses (the
+    plane kernel's per-lane counters are summed over the wave).  The plane
+    pass notices two equal determined cells in one unit only some passes
+    later (plane_solver.h), so it may branch inside an already-dead node the
+    wave kernel prunes: plane >= packed, by a hair."""
     from sudoku_solver_distributed_amd import _lib
     from sudoku_solver_distributed_amd.gen import hard17_batch
     p = hard17_batch(20000, seed=3).to(solver.device)
@@ -371,5 +374,6 @@ def test_stats_agree_between_kernels(solver):
     for k in ("packed", "plane"):
         assert got[k]["finished"] == 20000 and got[k]["solved"] == 20000, got
         assert got[k]["deferred"] == 0, got
-    assert got["plane"]["guesses"] == got["packed"]["guesses"], got
+    assert got["packed"]["guesses"] > 20000 * 0.3, got
+    assert got["packed"]["guesses"] <= got["plane"]["guesses"] <= got["packed"]["guesses"] * 1.01 + 16, got
     assert got["plane"]["sweeps"] > 20000 * 5, got
