@@ -90,10 +90,14 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
                         uint8_t *d_children, int64_t cap, int order, void *stream);
 
 /* Copy statistics to host (synchronous on `stream`):
- * out[0] boards finished, out[1] boards solved, out[2] guesses (DFS nodes),
- * out[3] propagation sweeps, out[4] lowest solved index in ordered mode
- * (INT64_MAX if none), out[5] boards the plane kernel handed to the
- * wave-per-board pass (clashing givens, searches deeper than its stack).  reset != 0 zeroes them afterwards. */
+ * out[0] boards finished, out[1] boards solved, out[2] guesses (branch
+ * nodes of the searches that gave each board its answer), out[3]
+ * propagation passes / sweeps executed (all work, including searches the
+ * plane kernel abandoned when it handed a board over), out[4] lowest solved
+ * index in ordered mode (INT64_MAX if none), out[5] boards the plane kernel
+ * handed to the wave-per-board pass (clashing givens, searches deeper than
+ * its stack, the last few boards of a wave once the queue is empty).
+ * reset != 0 zeroes them afterwards. */
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 
 /* Solve-kernel selection (library extension, no reference counterpart):

@@ -1,0 +1,42 @@
+"""Per-wave timeline of one plane_kernel launch (diagnostic build with
+SDK_PLANE_STAMPS=1, loaded with SDK_LIB=...libsudoku_hip_stamps.so).
+
+    SDK_LIB=$PWD/sudoku_solver_distributed_amd/libsudoku_hip_stamps.so python scripts/plane_timeline.py [BATCH]
+
+Prints, in microseconds from the first wave's start: when waves saw the
+queue drained and when they exited (percentiles over waves), and the loop
+iterations waves ran after the drain."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from sudoku_solver_distributed_amd.gen import hard17_batch  # noqa: E402
+from sudoku_solver_distributed_amd.solver import get_solver  # noqa: E402
+
+n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
+solver = get_solver("cuda:0")
+lib = solver.lib
+boards = hard17_batch(n, seed=2024, device="cuda:0")
+for _ in range(3):
+    solver.solve(boards)
+torch.cuda.synchronize()
+ws = solver.workspace
+cap = 1 << 20
+total = int(lib.sdk_workspace_bytes())
+list_off = total - cap * 8
+waves = (min(n, 256 * 4 * 256)) // 64
+st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 32].view(torch.int64).cpu().numpy().reshape(-1, 4)
+t0 = st[:, 0].min()
+us = lambda x: (x - t0) / 100.0  # 100 MHz
+q = [0, 10, 50, 90, 99, 100]
+print(f"batch {n}, waves {waves}")
+print("start   pct", q, np.percentile(us(st[:, 0]), q).round(1).tolist())
+print("drained pct", q, np.percentile(us(st[:, 1]), q).round(1).tolist())
+print("exit    pct", q, np.percentile(us(st[:, 2]), q).round(1).tolist())
+print("iters after drain pct", q, np.percentile(st[:, 3], q).round(0).tolist())
+ex = np.sort(us(st[:, 2]))
+for frac in (0.25, 0.5, 0.75, 0.9, 0.99):
+    print(f"  {frac:.0%} of waves exited by {ex[int(frac * (len(ex) - 1))]:.1f} us")

@@ -18,10 +18,12 @@
 // ---------------------------------------------------------------- workspace
 // word layout of the device workspace (uint64 words)
 enum {
-    WS_QUEUE = 0,      // chunked board queue head (re-armed every call)
-    WS_BEST = 1,       // ordered mode: lowest solved index (re-armed to INT64_MAX)
-    WS_ARM_WORDS = 2,  // words re-armed per call
-    WS_STACK_BYTE = 256,  // the plane kernel's per-lane stacks start here
+    WS_QUEUE = 0,        // chunked board queue head (re-armed every call)
+    WS_BEST = 1,         // ordered mode: lowest solved index (re-armed to INT64_MAX)
+    WS_DEFER_COUNT = 2,  // boards the plane kernel handed back (list entries, re-armed)
+    WS_DEFER_OVER = 3,   // 1: the list overflowed, every deferred board is found by status (re-armed)
+    WS_ARM_WORDS = 4,    // words re-armed per call
+    WS_STACK_BYTE = 256, // the plane kernel's per-lane stacks start here, then the deferred list
     WS_FINISHED = 8,   // statistics (accumulate until sdk_read_stats(reset))
     WS_SOLVED = 9,
     WS_GUESSES = 10,
@@ -51,11 +53,14 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
 
 // Launch the plane kernel (plane_kernels.hip) and report its occupancy.
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
-                            unsigned long long *ws, uint32_t *stack, int ordered, int order, int64_t threads,
-                            hipStream_t st);
+                            unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
+                            int64_t threads, hipStream_t st);
 int sdk_plane_blocks_per_cu();
 #define PLANE_MAX_DEPTH 32
 #define PLANE_THREADS 256
 #define PLANE_STACK_WORDS 28
+// board indices the plane kernel hands to the wave kernel (int64 each; more
+// than this and the wave kernel finds them by scanning the statuses)
+#define PLANE_DEFER_CAP (1 << 20)
 
 #endif  // SDK_COMMON_H

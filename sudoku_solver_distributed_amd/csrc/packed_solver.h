@@ -510,11 +510,12 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
 }
 
 // Second pass behind the plane kernel: solve exactly the boards it left
-// (status SDK_DEFERRED).  Each wave scans 64 statuses per load and runs the
-// deferred ones among them, grid-stride over the batch.
+// (status SDK_DEFERRED): the deferred list's entries, one board per wave,
+// grid-stride; if the list overflowed, every wave scans 64 statuses per load
+// instead and runs the deferred ones among them.
 __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep_deferred_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
-    int64_t n, unsigned long long *__restrict__ ws, int ordered, int order)
+    int64_t n, unsigned long long *__restrict__ ws, const int64_t *__restrict__ list, int ordered, int order)
 {
     __shared__ PackLds lds[WAVES_PER_BLOCK];
     const int lane = threadIdx.x & 63;
@@ -522,18 +523,30 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
     const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
     const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+    // both words were last written by the plane kernel (an earlier launch)
+    const int64_t cnt = (int64_t)ws[WS_DEFER_COUNT];
+    const bool over = ws[WS_DEFER_OVER] != 0;
+    if (cnt == 0 || (!over && gw >= cnt)) return;
 
     PCells s;
     pinit_lane(s, lane);
     uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
-    for (int64_t base = gw * 64; base < n; base += nwaves * 64) {
-        const int32_t sv = base + lane < n ? status[base + lane] : 0;
-        uint64_t m = __builtin_amdgcn_ballot_w64(sv == SDK_DEFERRED);
-        while (m) {
-            const int j = __builtin_ctzll(m);
-            m &= m - 1;
-            psolve_board(W, lane, s, puzzles, sols, status, base + j, ws, best, order, solved, guesses, sweeps);
+    if (!over) {
+        for (int64_t k = gw; k < cnt; k += nwaves) {
+            const int64_t p = list[k];
+            psolve_board(W, lane, s, puzzles, sols, status, p, ws, best, order, solved, guesses, sweeps);
             fin++;
+        }
+    } else {
+        for (int64_t base = gw * 64; base < n; base += nwaves * 64) {
+            const int32_t sv = base + lane < n ? status[base + lane] : 0;
+            uint64_t m = __builtin_amdgcn_ballot_w64(sv == SDK_DEFERRED);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                psolve_board(W, lane, s, puzzles, sols, status, base + j, ws, best, order, solved, guesses, sweeps);
+                fin++;
+            }
         }
     }
     pflush_stats(lane, ws, fin, solved, guesses, sweeps);

@@ -31,17 +31,20 @@
 
 #include "plane_solver.h"
 
+// defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
+// $SDK_PLANE_TAIL)
 #ifndef SDK_PLANE_REFILL
 #define SDK_PLANE_REFILL 12
 #endif
-// 1: test givens for repeated digits only when a search ends without a
-// completion (0: on every load, A/B)
-#ifndef SDK_PLANE_LAZY_CLASH
-#define SDK_PLANE_LAZY_CLASH 1
+#ifndef SDK_PLANE_TAIL
+#define SDK_PLANE_TAIL 0
 #endif
-// 1: each lane loads its own first board (lane-parallel start-up)
-#ifndef SDK_PLANE_LANE_START
-#define SDK_PLANE_LANE_START 1
+// diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
+// wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
+// plus the loop iterations after the drain, into the second half of the
+// deferred-list area (scripts/plane_timeline.py reads them)
+#ifndef SDK_PLANE_STAMPS
+#define SDK_PLANE_STAMPS 0
 #endif
 static_assert(PLANE_STACK_WORDS == plane::STACK_WORDS, "stack layout");
 
@@ -108,6 +111,17 @@ __device__ __forceinline__ bool plane_givens_clash(const uint8_t *__restrict__ s
     return plane::givens_clash(G, given);
 }
 
+// Hand board p to the wave kernel (status SDK_DEFERRED + an entry in the
+// deferred list; past PLANE_DEFER_CAP entries the wave kernel scans statuses).
+__device__ __forceinline__ void plane_defer(int64_t p, int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+                                            int64_t *__restrict__ list)
+{
+    status[p] = SDK_DEFERRED;
+    const unsigned long long k = atomicAdd(&ws[WS_DEFER_COUNT], 1ull);
+    if (k < (unsigned long long)PLANE_DEFER_CAP) list[k] = p;
+    else atomicOr(&ws[WS_DEFER_OVER], 1ull);
+}
+
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -129,7 +143,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 #endif
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
-    unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int ordered, int order)
+    unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
+    int order, int refill, int tail)
 {
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
@@ -147,9 +162,14 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // per-lane statistics (each lane counts its own boards' events; summed
     // over the wave at exit)
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
+    uint32_t bguess = 0;  // guesses on the current board (dropped if it is handed off)
     bool drained = false;  // the queue is empty
+#if SDK_PLANE_STAMPS
+    const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
+    uint64_t st_t1 = 0;
+    uint32_t st_after = 0;
+#endif
 
-#if SDK_PLANE_LANE_START
     // Start-up: every lane loads its own first board, all lanes and all 81
     // byte loads at once.  The cooperative refill below loads one board per
     // HBM round trip, which for a wave's first 64 boards is ~10 passes' time.
@@ -175,6 +195,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             if (ok && !cancel) {
                 p = q;
                 depth = 0;
+                bguess = 0;
                 state = PL_ACTIVE;
             } else {
                 for (int i = 0; i < 81; ++i) sols[q * 81 + i] = src[i];  // raw input back
@@ -182,11 +203,16 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             }
         }
     }
-#endif
 
     for (;;) {
+#if SDK_PLANE_STAMPS
+        if (drained) {
+            if (!st_t1) st_t1 = __builtin_amdgcn_s_memrealtime();
+            st_after++;
+        }
+#endif
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-        if (__builtin_popcountll(~active) >= SDK_PLANE_REFILL || active == 0) {
+        if (__builtin_popcountll(~active) >= refill || active == 0) {
             const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
             // ---- store finished boards, one at a time over the whole wave
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
@@ -231,8 +257,12 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     // unit: "no completion" is the packed kernel's call.  (A
                     // SOLVED result needs every unit to hold every digit, so
                     // such givens never reach the store above.)
-                    if (lane == 0) status[pi] = SDK_DEFERRED;
-                    if (lane == i) { fin--; deferred++; }
+                    if (lane == i) {
+                        plane_defer(pi, status, ws, defer_list);
+                        fin--;
+                        deferred++;
+                        guesses -= bguess;
+                    }
                     continue;
                 }
                 plane_copy_board(puzzles + pi * 81, sols + pi * 81, lane);
@@ -250,9 +280,6 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 base = __shfl(base, leader);
                 drained = (int64_t)base + k >= n;
                 bool loaded = false;
-#if !SDK_PLANE_LAZY_CLASH
-                uint32_t given[3] = {0u, 0u, 0u};
-#endif
                 m = idle;
                 for (int64_t q = (int64_t)base; m && q < n; ++q) {
                     const int i = __builtin_ctzll(m);
@@ -283,30 +310,28 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                         B.P[d][2] = lane == i ? (m1 | E[2]) : B.P[d][2];
                     }
                     if (lane == i) {
-#if !SDK_PLANE_LAZY_CLASH
-#pragma unroll
-                        for (int b = 0; b < 3; ++b) given[b] = plane::ROWS & ~E[b];
-#endif
                         B.Det[0] = B.Det[1] = B.Det[2] = 0;
                         p = q;
                         depth = 0;
+                        bguess = 0;
                         loaded = true;
                     }
                 }
-#if SDK_PLANE_LAZY_CLASH
                 if (loaded) state = PL_ACTIVE;
-#else
-                // eager variant (A/B): every loaded board's givens, lane-parallel
-                if (loaded) {
-                    if (plane::givens_clash(B, given)) {
-                        status[p] = SDK_DEFERRED;
-                        fin--;
-                        deferred++;
-                    } else {
-                        state = PL_ACTIVE;
-                    }
+            }
+            // ---- tail: the queue is empty and the wave is down to a few
+            // boards.  A pass costs the whole wave whatever its active
+            // lanes, so the wave would idle on its slowest board; the wave
+            // kernel solves each of them on a wave of its own instead.
+            if (drained) {
+                const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
+                if (act && __builtin_popcountll(act) <= tail && state == PL_ACTIVE) {
+                    plane_defer(p, status, ws, defer_list);
+                    fin--;
+                    deferred++;
+                    guesses -= bguess;
+                    state = PL_IDLE;
                 }
-#endif
             }
             if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;
         }
@@ -322,9 +347,10 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (r == plane::STUCK) {
             if (depth == PLANE_MAX_DEPTH) {
-                status[p] = SDK_DEFERRED;  // too deep for the stack: the packed kernel's
+                plane_defer(p, status, ws, defer_list);  // too deep for the stack: the wave kernel's
                 fin--;
                 deferred++;
+                guesses -= bguess;
                 state = PL_IDLE;
             } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
                 state = PL_CANCELLED;
@@ -338,6 +364,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 stk.put(depth, plane::STACK_ENTRY, plane::make_entry(band, pos, cand ^ d));
                 depth++;
                 guesses++;
+                bguess++;
                 plane::set_cell(B, band, pos, d);
             }
         } else if (r == plane::DEAD) {
@@ -358,11 +385,22 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 stk.put(depth, plane::STACK_ENTRY, e & ~(d << 8));
                 depth++;
                 guesses++;
+                bguess++;
                 plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
                 break;
             }
         }
     }
+#if SDK_PLANE_STAMPS
+    {
+        int64_t *st = defer_list + (PLANE_DEFER_CAP / 2) + 4 * (g >> 6);
+        const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
+        if (lane == 0) st[0] = (int64_t)st_t0;
+        if (lane == 1) st[1] = (int64_t)(st_t1 ? st_t1 : t2);
+        if (lane == 2) st[2] = (int64_t)t2;
+        if (lane == 3) st[3] = (int64_t)st_after;
+    }
+#endif
     // per-wave statistics: the lanes' counts summed, one atomic per counter and wave
     fin = wave_sum(fin);
     solved = wave_sum(solved);

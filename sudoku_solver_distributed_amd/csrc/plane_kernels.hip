@@ -3,16 +3,29 @@
 // machine scheduler; $SDK_PLANE_SCHED selects another strategy for A/B
 // builds).  The pass pins its board between digits (plane_solver.h PS_PIN),
 // which keeps it at ~113 VGPRs: four waves per SIMD, no spills.
+#include <stdlib.h>
+
 #include "common.h"
 #include "plane_kernel.h"
 
-hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
-                            unsigned long long *ws, uint32_t *stack, int ordered, int order, int64_t threads,
-                            hipStream_t st)
+// runtime tuning knobs (A/B without a rebuild): $SDK_PLANE_REFILL idle lanes
+// before a wave refills, $SDK_PLANE_TAIL active lanes at or below which a
+// wave hands its boards to the wave kernel once the queue is empty (0: off)
+static int env_int(const char *name, int dflt)
 {
+    const char *e = getenv(name);
+    return e && e[0] ? atoi(e) : dflt;
+}
+
+hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
+                            unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
+                            int64_t threads, hipStream_t st)
+{
+    static const int refill = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
+    static const int tail = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, ordered, order);
+                       stack, defer_list, ordered, order, refill, tail);
     return hipGetLastError();
 }
 

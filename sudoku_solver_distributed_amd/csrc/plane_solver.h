@@ -124,6 +124,12 @@ PS_FN int pass(Board &B, uint32_t und[3])
     uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
+        // hidden singles placed for digits < d this pass leave d's plane
+        // (Gauss-Seidel: d sees them); digits < d are fixed up after the loop
+        if (d > 0) {
+#pragma unroll
+            for (int b = 0; b < 3; ++b) B.P[d][b] &= ~hall[b];
+        }
         // ---- B: remove d from the peers of the newly determined cells holding d
         uint32_t x[3], f[3];
 #pragma unroll
@@ -160,17 +166,12 @@ PS_FN int pass(Board &B, uint32_t und[3])
         const uint32_t T = t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
         colall &= O;
         const uint32_t hcol = spread_rows(O & ~T);
-        // place d's hidden singles at once (Gauss-Seidel: later digits see
-        // them).  A cell forced for two digits loses the later one, whose
-        // unit then has no place for it: dead, as it must be.
+        // d's hidden singles: later digits drop these cells at their turn
+        // (above), earlier ones after the loop.  A cell forced for two
+        // digits loses the later one, whose unit then has no place for it:
+        // dead, as it must be.
 #pragma unroll
-        for (int b = 0; b < 3; ++b) {
-            const uint32_t h = hb[b] | (B.P[d][b] & hcol);
-            hall[b] |= h;
-#pragma unroll
-            for (int e = 0; e < 9; ++e)
-                if (e != d) B.P[e][b] &= ~h;
-        }
+        for (int b = 0; b < 3; ++b) hall[b] |= hb[b] | (B.P[d][b] & hcol);
         pin_board(B);
         // the unit accumulators too: unpinned, the AND / OR chains over the
         // nine digits are re-associated into trees at the end of the pass,
@@ -182,6 +183,19 @@ PS_FN int pass(Board &B, uint32_t und[3])
 #pragma unroll
         for (int b = 0; b < 3; ++b) PS_PIN(hall[b]);
 #endif
+    }
+    // A cell forced to digit d this pass is still in d's plane and, from the
+    // clearing above, in no later digit's: so it leaves every EARLIER plane
+    // that a later plane still holds.  Same state as clearing all eight
+    // other planes the moment d's singles were found.
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        uint32_t later = B.P[8][b];
+#pragma unroll
+        for (int e = 7; e >= 0; --e) {
+            B.P[e][b] &= ~(hall[b] & later);
+            if (e) later |= B.P[e][b];
+        }
     }
     dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;

@@ -68,6 +68,8 @@ __global__ void arm_kernel(unsigned long long *ws)
 {
     if (threadIdx.x == WS_QUEUE) ws[WS_QUEUE] = 0ull;
     if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
+    if (threadIdx.x == WS_DEFER_COUNT) ws[WS_DEFER_COUNT] = 0ull;
+    if (threadIdx.x == WS_DEFER_OVER) ws[WS_DEFER_OVER] = 0ull;
 }
 
 #include "packed_solver.h"
@@ -400,7 +402,10 @@ int sdk_set_solve_kernel(int kernel)
     g_variant.store(kernel ? kernel : env_variant());
     return prev;
 }
-size_t sdk_workspace_bytes(void) { return WS_STACK_BYTE + plane_stack_bytes(plane_max_threads()); }
+size_t sdk_workspace_bytes(void)
+{
+    return WS_STACK_BYTE + plane_stack_bytes(plane_max_threads()) + (size_t)PLANE_DEFER_CAP * sizeof(int64_t);
+}
 
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
                     void *d_workspace, int order, int ordered, void *stream)
@@ -432,14 +437,16 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
         const int64_t max_threads = plane_max_threads();
         const int64_t threads = n < max_threads ? n : max_threads;
         uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
-        e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, ordered, order, threads, st);
+        int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
+        e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, list, ordered, order, threads, st);
         if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
         // the boards it left (clashing givens, deep searches): wave per board
         const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_deferred_kernel, g_bpc_packed) * WAVES_PER_BLOCK;
         const int64_t groups = (n + 63) / 64;
         const int64_t waves = groups < max_waves ? groups : max_waves;
         hipLaunchKernelGGL(solvep_deferred_kernel, dim3((unsigned)((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
-                           dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions, d_status, n, ws, ordered, order);
+                           dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions, d_status, n, ws,
+                           (const int64_t *)list, ordered, order);
     }
     e = hipGetLastError();
     if (e != hipSuccess) return set_err("sdk_solve_batch: launch", e);

