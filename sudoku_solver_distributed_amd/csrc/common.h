@@ -51,6 +51,27 @@ __device__ __forceinline__ uint32_t rdlane(uint32_t v, int l)
     return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
 }
 
+__device__ __forceinline__ void cell_units(int cell, int &r, int &c, int &b)
+{
+    r = cell / 9;
+    c = cell - r * 9;
+    b = (r / 3) * 3 + c / 3;
+}
+
+// The walk's next cell among the empty cells {eb0 (cells 0..63), eb1 (64..80)},
+// not both zero.  Scalar bit work only.
+__device__ __forceinline__ int order_cell(uint64_t eb0, uint64_t eb1, int order)
+{
+    if (order == SDK_ORDER_NODE)  // node.py:63-65: row-major first
+        return eb0 ? __builtin_ctzll(eb0) : 64 + __builtin_ctzll(eb1);
+    // gen.py:11-15: last row holding an empty cell, its first empty column
+    const int hi = eb1 ? 64 + 63 - __builtin_clzll(eb1) : 63 - __builtin_clzll(eb0);
+    const int start = (hi / 9) * 9;
+    if (start >= 64) return start + __builtin_ctzll(eb1 >> (start - 64));
+    const uint64_t m = eb0 & (~0ull << start);
+    return m ? __builtin_ctzll(m) : 64 + __builtin_ctzll(eb1);
+}
+
 // Launch the plane kernel (plane_kernels.hip) and report its occupancy.
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
                             unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,

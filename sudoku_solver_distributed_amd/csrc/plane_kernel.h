@@ -30,6 +30,7 @@
 #define SDK_PLANE_KERNEL_H
 
 #include "plane_solver.h"
+#include "packed_solver.h"
 
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
 // $SDK_PLANE_TAIL)
@@ -37,7 +38,7 @@
 #define SDK_PLANE_REFILL 12
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 0
+#define SDK_PLANE_TAIL 2
 #endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
@@ -122,6 +123,29 @@ __device__ __forceinline__ void plane_defer(int64_t p, int32_t *__restrict__ sta
     else atomicOr(&ws[WS_DEFER_OVER], 1ull);
 }
 
+// A drained wave's last boards (lanes `act`, board index p_lo / p_hi per
+// lane), each restarted on the whole wave by the wave-per-board solver.  Runs
+// after the pass loop, so the planes' registers are free for it.
+// st: solved, guesses, sweeps (wave-uniform).
+__device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, uint32_t p_lo, uint32_t p_hi,
+                                        const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols,
+                                        int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+                                        const int64_t *best, int order, uint32_t (&st)[3])
+{
+    PCells cs;
+    pinit_lane(cs, lane);
+    uint32_t solved = 0, guesses = 0, sweeps = 0;
+    while (act) {
+        const int i = __builtin_ctzll(act);
+        act &= act - 1;
+        const int64_t pi = ((int64_t)rdlane(p_hi, i) << 32) | rdlane(p_lo, i);
+        psolve_board(W, lane, cs, puzzles, sols, status, pi, ws, best, order, solved, guesses, sweeps);
+    }
+    st[0] = solved;
+    st[1] = guesses;
+    st[2] = sweeps;
+}
+
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -146,6 +170,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
     int order, int refill, int tail)
 {
+    __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
     const PlaneStack stk = {
@@ -164,6 +189,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     uint32_t bguess = 0;  // guesses on the current board (dropped if it is handed off)
     bool drained = false;  // the queue is empty
+    uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
 #if SDK_PLANE_STAMPS
     const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t st_t1 = 0;
@@ -321,16 +347,16 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             }
             // ---- tail: the queue is empty and the wave is down to a few
             // boards.  A pass costs the whole wave whatever its active
-            // lanes, so the wave would idle on its slowest board; the wave
-            // kernel solves each of them on a wave of its own instead.
-            if (drained) {
+            // lanes, so the wave would idle on its slowest board for tens of
+            // passes; instead it restarts each of them on the wave-per-board
+            // solver (packed_solver.h, ~one pass's worth of instructions per
+            // board) and exits.
+            if (drained && tail > 0) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                if (act && __builtin_popcountll(act) <= tail && state == PL_ACTIVE) {
-                    plane_defer(p, status, ws, defer_list);
-                    fin--;
-                    deferred++;
-                    guesses -= bguess;
-                    state = PL_IDLE;
+                if (act && __builtin_popcountll(act) <= tail) {
+                    if (state == PL_ACTIVE) guesses -= bguess;  // those searches start over
+                    tail_act = act;
+                    break;
                 }
             }
             if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;
@@ -389,6 +415,17 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
                 break;
             }
+        }
+    }
+    if (tail_act) {
+        // after the loop: the planes are dead, the wave solver gets the registers
+        uint32_t wst[3];
+        plane_tail(tail_lds[threadIdx.x >> 6], lane, tail_act, (uint32_t)p, (uint32_t)(p >> 32), puzzles, sols,
+                   status, ws, best, order, wst);
+        if (lane == 0) {
+            solved += wst[0];
+            guesses += wst[1];
+            passes += wst[2];
         }
     }
 #if SDK_PLANE_STAMPS

@@ -10,7 +10,8 @@
 
 // runtime tuning knobs (A/B without a rebuild): $SDK_PLANE_REFILL idle lanes
 // before a wave refills, $SDK_PLANE_TAIL active lanes at or below which a
-// wave hands its boards to the wave kernel once the queue is empty (0: off)
+// wave restarts its last boards on the wave-per-board solver once the queue
+// is empty (0: off)
 static int env_int(const char *name, int dflt)
 {
     const char *e = getenv(name);

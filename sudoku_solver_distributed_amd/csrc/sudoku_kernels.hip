@@ -41,27 +41,6 @@
 #define SDK_PLANE_MIN_BATCH 8192
 #endif
 
-__device__ __forceinline__ void cell_units(int cell, int &r, int &c, int &b)
-{
-    r = cell / 9;
-    c = cell - r * 9;
-    b = (r / 3) * 3 + c / 3;
-}
-
-// The walk's next cell among the empty cells {eb0 (cells 0..63), eb1 (64..80)},
-// not both zero.  Scalar bit work only.
-__device__ __forceinline__ int order_cell(uint64_t eb0, uint64_t eb1, int order)
-{
-    if (order == SDK_ORDER_NODE)  // node.py:63-65: row-major first
-        return eb0 ? __builtin_ctzll(eb0) : 64 + __builtin_ctzll(eb1);
-    // gen.py:11-15: last row holding an empty cell, its first empty column
-    const int hi = eb1 ? 64 + 63 - __builtin_clzll(eb1) : 63 - __builtin_clzll(eb0);
-    const int start = (hi / 9) * 9;
-    if (start >= 64) return start + __builtin_ctzll(eb1 >> (start - 64));
-    const uint64_t m = eb0 & (~0ull << start);
-    return m ? __builtin_ctzll(m) : 64 + __builtin_ctzll(eb1);
-}
-
 // ------------------------------------------------------------- solve kernel
 // re-arm the per-call workspace words on the stream (graph-capturable)
 __global__ void arm_kernel(unsigned long long *ws)
@@ -73,6 +52,83 @@ __global__ void arm_kernel(unsigned long long *ws)
 }
 
 #include "packed_solver.h"
+
+#ifndef SDK_PACKED_WAVES_PER_EU
+#define SDK_PACKED_WAVES_PER_EU 1
+#endif
+__global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, int64_t chunk, int ordered, int order)
+{
+    __shared__ PackLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    PackLds &W = lds[threadIdx.x >> 6];
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+
+    PCells s;
+    pinit_lane(s, lane);
+    uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
+    // first chunk statically, the rest from the queue
+    int64_t base = gw * chunk;
+    const int64_t static_end = nwaves * chunk;
+    while (base < n) {
+        const int64_t end = base + chunk < n ? base + chunk : n;
+        for (int64_t p = base; p < end; ++p) {
+            psolve_board(W, lane, s, puzzles, sols, status, p, ws, best, order, solved, guesses, sweeps);
+            fin++;
+        }
+        unsigned long long t = 0;
+        if (lane == 0) t = atomicAdd(&ws[WS_QUEUE], 1ull);
+        t = __shfl(t, 0);
+        base = static_end + (int64_t)t * chunk;
+    }
+    pflush_stats(lane, ws, fin, solved, guesses, sweeps);
+}
+
+// Second pass behind the plane kernel: solve exactly the boards it left
+// (status SDK_DEFERRED): the deferred list's entries, one board per wave,
+// grid-stride; if the list overflowed, every wave scans 64 statuses per load
+// instead and runs the deferred ones among them.
+__global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep_deferred_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status,
+    int64_t n, unsigned long long *__restrict__ ws, const int64_t *__restrict__ list, int ordered, int order)
+{
+    __shared__ PackLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    PackLds &W = lds[threadIdx.x >> 6];
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
+    // both words were last written by the plane kernel (an earlier launch)
+    const int64_t cnt = (int64_t)ws[WS_DEFER_COUNT];
+    const bool over = ws[WS_DEFER_OVER] != 0;
+    if (cnt == 0 || (!over && gw >= cnt)) return;
+
+    PCells s;
+    pinit_lane(s, lane);
+    uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
+    if (!over) {
+        for (int64_t k = gw; k < cnt; k += nwaves) {
+            const int64_t p = list[k];
+            psolve_board(W, lane, s, puzzles, sols, status, p, ws, best, order, solved, guesses, sweeps);
+            fin++;
+        }
+    } else {
+        for (int64_t base = gw * 64; base < n; base += nwaves * 64) {
+            const int32_t sv = base + lane < n ? status[base + lane] : 0;
+            uint64_t m = __builtin_amdgcn_ballot_w64(sv == SDK_DEFERRED);
+            while (m) {
+                const int j = __builtin_ctzll(m);
+                m &= m - 1;
+                psolve_board(W, lane, s, puzzles, sols, status, base + j, ws, best, order, solved, guesses, sweeps);
+                fin++;
+            }
+        }
+    }
+    pflush_stats(lane, ws, fin, solved, guesses, sweeps);
+}
 
 // ------------------------------------------------------------ check kernel
 // One thread per grid; the block stages its 64 grids (5184 B) through LDS
