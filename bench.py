@@ -16,7 +16,8 @@ Rank 0 prints ONE JSON line with the contract fields plus:
                   algorithmic bytes per launch against HBM;
   cpu_baseline -- the oracle's literal reference walk (gen.py:6-28 restated in
                   C, oracle/) on a time-bounded sample of the same boards, one
-                  host core, rank 0 at N = 1 only;
+                  walk per host core (affinity, capped by $OMP_NUM_THREADS),
+                  rank 0 at N = 1 only;
   p50_single_ms -- single-board latency (one board per launch, frontier
                   split off), median over the first boards of the batch.
 """
@@ -38,11 +39,14 @@ PMC_DIR = os.path.join(ROOT, "profiles")   # pmc_<kernel symbol>.json (scripts/g
 
 
 def cpu_baseline(boards, budget_s: float):
-    """Literal reference walk on one core; boards completed within budget."""
+    """Literal reference walk (gen.py:6-28 restated in C, oracle/) on every
+    host core this process may use, one walk per core over its own slice of
+    the sample; boards completed within the budget."""
     from oracle import oracle as O  # checker only: bench's cpu_baseline leg
+    threads = O.host_threads()
     t0 = time.perf_counter()
-    done, _, _ = O.solve_batch_timed(boards, budget_s)
-    return done, time.perf_counter() - t0
+    done = O.solve_batch_timed_parallel(boards, budget_s, threads)
+    return done, time.perf_counter() - t0, threads
 
 
 def _time(fn, reps=3):
@@ -200,11 +204,12 @@ def main():
 
     cpu = None
     if world == 1 and not args.no_cpu:
-        sample = boards[:4096].cpu().numpy()
-        done, el = cpu_baseline(sample, args.cpu_budget)
-        cpu = {"value": done / el, "unit": "boards/s", "cores": 1, "kind": "port",
-               "sample": f"first {done} boards of the same hard-17 batch completed in {el:.1f} s "
-                         f"(literal gen.py:6-28 walk, oracle/sudoku_oracle.c, 1 thread)"}
+        sample = boards[:8192].cpu().numpy()
+        done, el, threads = cpu_baseline(sample, args.cpu_budget)
+        cpu = {"value": done / el, "unit": "boards/s", "cores": threads, "kind": "port",
+               "sample": f"{done} boards of the same hard-17 batch (first 8192, split into {threads} "
+                         f"contiguous slices) completed in {el:.1f} s by {threads} host threads, one "
+                         f"literal gen.py:6-28 walk each (oracle/sudoku_oracle.c)"}
 
     line = {
         "metric": "puzzles solved/sec (node), 1M hard 9x9 batch @1/2/4/8 GPU; single-puzzle p50 ms",

@@ -111,7 +111,7 @@ int oracle_is_valid_move(const uint8_t *g, int row, int col, int num)
 
 typedef int (*valid_fn)(const uint8_t *, int, int, int);
 
-static uint64_t g_nodes; /* candidate tests (the reference's "validations") */
+static _Thread_local uint64_t g_nodes; /* candidate tests (the reference's "validations"), per thread */
 
 /* gen.py:11-15: `for i: for j: if empty: row, col = i, j; break` -- the
  * break leaves only the column loop, so the LAST row with an empty cell wins,
@@ -354,8 +354,8 @@ void oracle_solve_unique_batch(const uint8_t *in, uint8_t *out, int32_t *count, 
  * `seconds` of wall time have elapsed; returns the number of boards fully
  * solved (a board cut off by the deadline is not counted). */
 #include <time.h>
-static double g_deadline;
-static int g_abort;
+static _Thread_local double g_deadline; /* per thread: bench.py runs one walk per host core */
+static _Thread_local int g_abort;
 
 static double now_s(void)
 {

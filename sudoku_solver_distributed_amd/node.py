@@ -2,7 +2,8 @@
 (`/solve`, `/stats`, `/network`) and a UDP JSON protocol between peers,
 whose Sudoku work runs on the GPU(s) the peer owns.
 
-    python -m sudoku_solver_distributed_amd.node -p 8000 -s 7000 [-a host:port] [-h 0] [--host 127.0.0.1]
+    python -m sudoku_solver_distributed_amd.node -p 8000 -s 7000 [-a host:port] [-h 0]
+           [--host 127.0.0.1] [--gpus 0,1] [--forward-threshold N]
 
 What changed against node.py (and why):
 
@@ -11,16 +12,31 @@ What changed against node.py (and why):
   check (node.py:82-116) and the per-cell task (`solve_sudoku_destributed`,
   node.py:76-80) are HIP kernels.  `validations` counts what the reference
   counts (one per check() call) plus, for a GPU solve, the kernel's
-  propagation sweeps (each one validates every empty cell once).
-* ``P2PNode.peer_sudoku_solve`` (node.py:534-557) no longer farms cells out
-  to UDP peers one at a time (node.py:427-475): the board is solved by this
-  peer's GPUs, bit-identical to node.py's recursive walk.  The UDP `solve` /
-  `solution` messages (node.py:384-406) are kept: with `row`/`col` they are
-  the reference's cell task; without them a peer may hand a whole board
-  (or a batch, `"sudokus"`) to another peer.
+  propagation passes (each one validates every empty cell once).
+* Every board a peer is asked to solve -- HTTP `/solve` (node.py:672-690),
+  a UDP `solve` message, `SudokuSolver.solve_sudoku` -- goes through one
+  ``BoardBatcher`` per peer: concurrent requests are coalesced into one GPU
+  launch per tick (``max_wait`` after the first pending board, or
+  ``max_batch`` boards), sharded over the peer's GPUs (``GpuSolverBackend``),
+  and each request gets its own board back.  This is what makes a peer
+  serve many clients at once (BASELINE.json configs[4]).
+* ``P2PNode.peer_sudoku_solve`` (node.py:534-557) no longer deals one
+  board's empty cells to peers one UDP message each (node.py:419-475): a
+  board is a few microseconds of GPU work, so the unit of distribution is a
+  whole board.  A peer whose batcher queue holds ``forward_threshold`` boards
+  or more hands new boards to its peers (round robin, UDP `solve` with a
+  `task` id, answered by a `solution` message) and solves locally if a peer
+  does not answer in time.  The answer is node.py's recursive walk
+  (node.py:62-74), bit-identical; the reference's HTTP path answers with its
+  greedy task loop instead, which differs on some boards (INTEGRATION.md §3,
+  tests/golden/golden_peer.json).
+* The UDP `solve` / `solution` messages (node.py:384-406) are kept: with
+  `row`/`col` they are the reference's cell task; without them a peer hands
+  a whole board (`sudoku`) or a batch (`sudokus`, 81-character strings).
 * Membership and statistics messages (`connect`, `connected`, `all_peers`,
   `disconnect`, `stats`; node.py:193-382) keep their JSON shape.
-* The HTTP server binds a configurable host (node.py:708 hard-codes a LAN IP).
+* The HTTP server binds a configurable host (node.py:708 hard-codes a LAN IP)
+  and serves requests on threads.
 """
 from __future__ import annotations
 
@@ -32,8 +48,9 @@ import socket
 import threading
 import time
 from collections import deque
+from concurrent.futures import Future
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
-from typing import Optional
+from typing import List, Optional
 
 import torch
 
@@ -48,34 +65,138 @@ class GpuSolverBackend:
     def __init__(self, devices=None):
         if devices is None:
             devices = [torch.cuda.current_device()] if torch.cuda.is_available() else [None]
-        self.solvers = [get_solver(d) for d in devices]
+        solvers = {}
+        for d in devices:
+            s = get_solver(d)
+            solvers[s.device.index] = s
+        self.solvers = [solvers[k] for k in sorted(solvers)]  # lock order: device index
 
     def solve(self, boards: torch.Tensor, order: str):
+        """(n,81) host boards -> (host solutions, host status, passes).  Each
+        device's op_lock is held from the pass-counter read before the launch
+        to the one after it, so other users of the device (another peer in
+        this process) neither interleave launches nor leak into the count."""
         boards = as_boards(boards)
         n = boards.shape[0]
         k = len(self.solvers)
         parts = [boards[i * n // k:(i + 1) * n // k] for i in range(k)]
-        outs = []
-        sweeps = 0
-        for s, part in zip(self.solvers, parts):  # launches are asynchronous per device
-            s.stats(reset=True)
-            outs.append(s.solve(part, order=order) if part.shape[0] else None)
-        sols, st = [], []
-        for s, o in zip(self.solvers, outs):
-            if o is None:
-                continue
-            sols.append(o[0].cpu())
-            st.append(o[1].cpu())
-            sweeps += s.stats()["sweeps"]
+        for s in self.solvers:
+            s.op_lock.acquire()
+        try:
+            outs = []
+            for s, part in zip(self.solvers, parts):  # launches are asynchronous per device
+                if part.shape[0] == 0:
+                    outs.append(None)
+                    continue
+                before = s.stats()["sweeps"]
+                outs.append((s.solve(part, order=order), before))
+            sols, st, sweeps = [], [], 0
+            for s, o in zip(self.solvers, outs):
+                if o is None:
+                    continue
+                (sol, stt), before = o
+                sols.append(sol.cpu())
+                st.append(stt.cpu())
+                sweeps += s.stats()["sweeps"] - before
+        finally:
+            for s in reversed(self.solvers):
+                s.op_lock.release()
         if not sols:
             return torch.empty((0, 81), dtype=torch.uint8), torch.empty(0, dtype=torch.int32), 0
         return torch.cat(sols), torch.cat(st), sweeps
 
     def check(self, boards, mode: int):
-        return self.solvers[0].check(as_boards(boards), mode).cpu()
+        return self.solvers[0].check(as_boards(boards, max_value=255), mode).cpu()
 
     def first_candidate(self, boards, cells):
-        return self.solvers[0].first_candidate(as_boards(boards), cells).cpu()
+        return self.solvers[0].first_candidate(as_boards(boards, max_value=255), cells).cpu()
+
+
+class BoardBatcher:
+    """Coalesces concurrent solve requests into one backend call per tick.
+
+    submit() queues (n, 81) boards with a walk order and returns a Future of
+    (solutions, status); one thread drains the queue: it waits for the first
+    board, then up to ``max_wait`` seconds (or until ``max_batch`` boards are
+    queued) for more, and solves each order's boards in one call."""
+
+    def __init__(self, backend, max_batch: int = 1 << 16, max_wait: float = 0.0005, on_batch=None):
+        self.backend = backend
+        self.max_batch = max_batch
+        self.max_wait = max_wait
+        self.on_batch = on_batch  # callback(boards, passes) after each backend call
+        self._q = deque()
+        self._queued = 0
+        self._cv = threading.Condition()
+        self._stop = False
+        self.batches = 0
+        self.boards = 0
+        self._thread = threading.Thread(target=self._run, name="BoardBatcher", daemon=True)
+        self._thread.start()
+
+    def pending(self) -> int:
+        return self._queued
+
+    def submit(self, boards: torch.Tensor, order: str = "node") -> Future:
+        boards = as_boards(boards)
+        fut: Future = Future()
+        with self._cv:
+            if self._stop:
+                raise RuntimeError("BoardBatcher is closed")
+            self._q.append((boards, order, fut))
+            self._queued += boards.shape[0]
+            self._cv.notify()
+        return fut
+
+    def close(self):
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        self._thread.join(timeout=5)
+
+    def _take(self):
+        with self._cv:
+            while not self._q and not self._stop:
+                self._cv.wait()
+            if self._stop and not self._q:
+                return None
+            deadline = time.monotonic() + self.max_wait
+            while self._queued < self.max_batch and not self._stop:
+                left = deadline - time.monotonic()
+                if left <= 0:
+                    break
+                self._cv.wait(left)
+            items, n = [], 0
+            while self._q and (n == 0 or n + self._q[0][0].shape[0] <= self.max_batch):
+                it = self._q.popleft()
+                items.append(it)
+                n += it[0].shape[0]
+            self._queued -= n
+            return items
+
+    def _run(self):
+        while True:
+            items = self._take()
+            if items is None:
+                return
+            for order in sorted({it[1] for it in items}):
+                group = [it for it in items if it[1] == order]
+                try:
+                    boards = torch.cat([it[0] for it in group])
+                    sols, st, passes = self.backend.solve(boards, order)
+                    self.batches += 1
+                    self.boards += boards.shape[0]
+                    if self.on_batch is not None:
+                        self.on_batch(boards.shape[0], int(passes))
+                    lo = 0
+                    for b, _, fut in group:
+                        hi = lo + b.shape[0]
+                        fut.set_result((sols[lo:hi], st[lo:hi]))
+                        lo = hi
+                except Exception as e:  # every waiter hears about it
+                    for _, _, fut in group:
+                        if not fut.done():
+                            fut.set_exception(e)
 
 
 def _flat(board):
@@ -90,7 +211,7 @@ def _copy_into(board, flat):
 class SudokuSolver:
     """node.py:21-131 with the walk, check and cell task on the GPU."""
 
-    def __init__(self, base_delay=0.01, backend=None):
+    def __init__(self, base_delay=0.01, backend=None, max_wait: float = 0.0005):
         logger.info("Initializing Sudoku solver")
         self.sudoku_board = None
         self.recent_requests = deque()
@@ -99,13 +220,21 @@ class SudokuSolver:
         self.base_delay = base_delay
         self.backend = backend if backend is not None else GpuSolverBackend()
         self.lock = threading.Lock()
+        self.batcher = BoardBatcher(self.backend, max_wait=max_wait, on_batch=self._count_passes)
 
-    # node.py:31-40
+    def _count_passes(self, boards, passes):
+        with self.lock:
+            self.validations += passes
+
+    # node.py:31-40 (returns the caller's board object, which node.py keeps
+    # in self.sudoku_board -- under concurrent requests that attribute is the
+    # latest request's, so it is not read back)
     def solve_sudoku(self, sudoku):
         self.sudoku_board = sudoku
-        if self.solve_sudoku_recursive(self.sudoku_board):
-            self.solved_puzzles += 1
-            return self.sudoku_board
+        if self.solve_sudoku_recursive(sudoku):
+            with self.lock:
+                self.solved_puzzles += 1
+            return sudoku
         logger.error("Failed to solve Sudoku puzzle")
         return None
 
@@ -125,9 +254,7 @@ class SudokuSolver:
 
     # node.py:62-74 -- the walk in node order, on the GPU, board filled in place
     def solve_sudoku_recursive(self, board):
-        sols, st, sweeps = self.backend.solve(as_boards(_flat(board)), "node")
-        with self.lock:
-            self.validations += int(sweeps)
+        sols, st = self.batcher.submit(as_boards(_flat(board)), "node").result()
         if int(st[0]) != SDK_SOLVED:
             return False
         _copy_into(board, sols[0].tolist())
@@ -135,16 +262,15 @@ class SudokuSolver:
 
     # node.py:76-80 -- the UDP "solve" cell task
     def solve_sudoku_destributed(self, board, row, col):
-        num = int(self.backend.first_candidate(as_boards(_flat(board)), [row * 9 + col])[0])
+        num = int(self.backend.first_candidate(as_boards(_flat(board), max_value=255), [row * 9 + col])[0])
         with self.lock:
             self.validations += 1
         return num if num > 0 else None
 
     def solve_many(self, boards, order="node"):
         """Batch entry point (no reference counterpart): (n,81) -> (sols, status)."""
-        sols, st, sweeps = self.backend.solve(as_boards(boards), order)
+        sols, st = self.batcher.submit(as_boards(boards), order).result()
         with self.lock:
-            self.validations += int(sweeps)
             self.solved_puzzles += int((st == SDK_SOLVED).sum())
         return sols, st
 
@@ -152,14 +278,14 @@ class SudokuSolver:
     def check(self, board, interval=10, threshold=5):
         with self.lock:
             self.validations += 1
-        now = time.time()
-        self.recent_requests.append(now)
-        while self.recent_requests and now - self.recent_requests[0] >= interval:
-            self.recent_requests.popleft()
-        n = len(self.recent_requests)
+            now = time.time()
+            self.recent_requests.append(now)
+            while self.recent_requests and now - self.recent_requests[0] >= interval:
+                self.recent_requests.popleft()
+            n = len(self.recent_requests)
         if n > threshold and self.base_delay:
             time.sleep(self.base_delay * (n - threshold + 1))
-        return bool(int(self.backend.check(as_boards(_flat(board)), 1)[0]))
+        return bool(int(self.backend.check(as_boards(_flat(board), max_value=255), 1)[0]))
 
     # node.py:118-131
     def __str__(self, board=None):
@@ -175,12 +301,21 @@ class SudokuSolver:
             out += "\n"
         return out
 
+    def close(self):
+        self.batcher.close()
+
+
+def _s81(board) -> str:
+    return "".join(str(int(v)) for v in (_flat(board) if isinstance(board[0], list) else board))
+
 
 class P2PNode:
     """node.py:134-657: UDP JSON peer + statistics; solving on local GPUs."""
 
-    def __init__(self, host, port, anchor_node=None, handicap=0.001, backend=None):
-        self.solver = SudokuSolver(handicap, backend=backend)
+    def __init__(self, host, port, anchor_node=None, handicap=0.001, backend=None,
+                 forward_threshold: Optional[int] = None, forward_timeout: float = 10.0,
+                 max_wait: float = 0.0005):
+        self.solver = SudokuSolver(handicap, backend=backend, max_wait=max_wait)
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         self.sock.settimeout(0.2)
         self.id = f"{host}:{port}"
@@ -193,8 +328,14 @@ class P2PNode:
         self.total_peers = []
         self.stats_solved = {}
         self.all_stats = {"all": {"solved": 0, "validations": 0}, "nodes": []}
+        self.forward_threshold = forward_threshold
+        self.forward_timeout = forward_timeout
+        self.forwarded = 0       # boards this peer handed to others
+        self.served = 0          # boards this peer solved for others
+        self._rr = itertools.count()
         self._tasks = {}         # task id -> [threading.Event, reply]
         self._task_ids = itertools.count(1)
+        self._stats_timer = None
         self.lock = threading.RLock()
 
     # ---------------------------------------------------------- transport
@@ -214,19 +355,41 @@ class P2PNode:
             return None, None
 
     def connected_peers(self):
-        return sorted(self.peers_out | self.peers_in)
+        with self.lock:
+            return sorted(self.peers_out | self.peers_in)
 
     def broadcast(self, msg):
         for peer in self.connected_peers():
             self.send(peer, msg)
 
     def broadcast_all_peers(self):
-        self.broadcast({"type": "all_peers", "all_peers": self.all_peers})
+        with self.lock:
+            msg = {"type": "all_peers", "all_peers": {k: list(v) for k, v in self.all_peers.items()}}
+        self.broadcast(msg)
+
+    def broadcast_stats_soon(self, delay: float = 0.02):
+        """broadcast_stats at most once per `delay` under load: one gossip
+        round covers every request finished meanwhile."""
+        with self.lock:
+            if self._stats_timer is not None:
+                return
+            self._stats_timer = threading.Timer(delay, self._stats_tick)
+            self._stats_timer.daemon = True
+            self._stats_timer.start()
+
+    def _stats_tick(self):
+        with self.lock:
+            self._stats_timer = None
+        if not self.shutdown_flag:
+            self.broadcast_stats()
 
     def broadcast_stats(self):
-        self.broadcast({"type": "stats", "origin": self.id, "solved": self.solver.solved_puzzles,
-                        "stats": {"address": self.id, "validations": self.solver.validations},
-                        "all_stats": self.get_stats()})
+        stats = self.get_stats()
+        with self.solver.lock:
+            solved, validations = self.solver.solved_puzzles, self.solver.validations
+        self.broadcast({"type": "stats", "origin": self.id, "solved": solved,
+                        "stats": {"address": self.id, "validations": validations},
+                        "all_stats": stats})
 
     def _refresh_total_peers(self):
         peers = set(self.all_peers)
@@ -238,6 +401,10 @@ class P2PNode:
     # ----------------------------------------------------------- messages
     def handle_message(self, msg):
         t = msg.get("type")
+        if t == "solve":  # GPU work off the receive loop
+            threading.Thread(target=self._handle_solve, args=(msg,), daemon=True).start()
+            return
+        rebroadcast = False
         with self.lock:
             if t == "connect":  # node.py:195-199
                 self.peers_out.add(msg["address"])
@@ -246,26 +413,26 @@ class P2PNode:
                 self.peers_in.add(msg["address"])
                 self.all_peers[msg["address"]] = sorted(set(self.all_peers.get(msg["address"], [])) | {self.id})
                 self._refresh_total_peers()
-                self.broadcast_all_peers()
+                rebroadcast = True
             elif t == "all_peers":  # node.py:213-260 (merge, re-broadcast on change)
-                changed = False
                 for peer, kids in msg["all_peers"].items():
                     merged = sorted(set(self.all_peers.get(peer, [])) | set(kids))
                     if merged != self.all_peers.get(peer):
                         self.all_peers[peer] = merged
-                        changed = True
+                        rebroadcast = True
                 self._refresh_total_peers()
-                if changed:
-                    self.broadcast_all_peers()
-                    self.broadcast_stats()
             elif t == "stats":  # node.py:264-331 (max-merge per node)
                 addr = msg["stats"]["address"]
-                if msg.get("solved", 0):
-                    self.stats_solved[addr] = max(self.stats_solved.get(addr, 0), msg["solved"])
-                self._merge_node(addr, msg["stats"]["validations"])
+                changed = self._merge_solved(addr, msg.get("solved", 0))
+                changed |= self._merge_node(addr, msg["stats"]["validations"])
                 for node in msg.get("all_stats", {}).get("nodes", []):
                     if node["address"] != self.id:
-                        self._merge_node(node["address"], node["validations"])
+                        changed |= self._merge_node(node["address"], node["validations"])
+                for node in msg.get("all_stats", {}).get("solved_by", []):
+                    if node["address"] != self.id:
+                        changed |= self._merge_solved(node["address"], node["solved"])
+                if changed:  # pass news on (peers are not all connected to each other)
+                    self.broadcast_stats_soon()
             elif t == "disconnect":  # node.py:334-381
                 a = msg["address"]
                 self.peers_in.discard(a)
@@ -283,41 +450,65 @@ class P2PNode:
                 if task is not None:
                     task[1] = msg
                     task[0].set()
-        if t == "solve":
-            self._handle_solve(msg)
+        if rebroadcast:
+            self.broadcast_all_peers()
+            self.broadcast_stats()
 
-    def _merge_node(self, addr, validations):
+    def _merge_node(self, addr, validations) -> bool:
         for node in self.all_stats["nodes"]:
             if node["address"] == addr:
-                node["validations"] = max(node["validations"], validations)
-                return
+                if validations > node["validations"]:
+                    node["validations"] = validations
+                    return True
+                return False
         self.all_stats["nodes"].append({"address": addr, "validations": validations})
+        return True
+
+    def _merge_solved(self, addr, solved) -> bool:
+        if solved and solved > self.stats_solved.get(addr, 0):
+            self.stats_solved[addr] = solved
+            return True
+        return False
 
     def _handle_solve(self, msg):
-        sudoku = msg["sudoku"]
+        sudoku = msg.get("sudoku")
         if "row" in msg and "col" in msg:  # node.py:384-406: the cell task
             num = self.solver.solve_sudoku_destributed(sudoku, msg["row"], msg["col"])
             reply = {"type": "solution", "sudoku": sudoku, "row": msg["row"], "col": msg["col"],
                      "solution": num, "address": self.id}
-        elif "sudokus" in msg:  # a batch handed over by a peer
-            sols, st = self.solver.solve_many(torch.tensor(msg["sudokus"], dtype=torch.uint8).reshape(-1, 81))
-            reply = {"type": "solution", "sudokus": sols.tolist(), "status": st.tolist(), "address": self.id}
+        elif "sudokus" in msg:  # a batch handed over by a peer (81-character strings)
+            boards = torch.tensor([[int(c) for c in s] for s in msg["sudokus"]], dtype=torch.uint8).reshape(-1, 81)
+            sols, st = self.solver.solve_many(boards, order=msg.get("order", "node"))
+            with self.lock:
+                self.served += boards.shape[0]
+            reply = {"type": "solution", "sudokus": ["".join(map(str, r.tolist())) for r in sols],
+                     "status": st.tolist(), "address": self.id}
         else:  # a whole board handed over by a peer
             board = [row[:] for row in sudoku]
             out = self.solver.solve_sudoku(board)
+            with self.lock:
+                self.served += 1
             reply = {"type": "solution", "sudoku": board, "solved": out is not None, "address": self.id}
         if "task" in msg:
             reply["task"] = msg["task"]
         self.send(msg["address"], reply)
-        self.broadcast_stats()
+        self.broadcast_stats_soon()
 
     def request_solve(self, peer, sudoku, timeout=10.0):
         """Hand a whole board to `peer` over UDP and wait for its solution."""
+        return self._request(peer, {"type": "solve", "sudoku": sudoku}, timeout)
+
+    def request_solve_many(self, peer, boards81: List[str], order="node", timeout=10.0):
+        """Hand a batch of boards (81-character strings) to `peer`."""
+        return self._request(peer, {"type": "solve", "sudokus": list(boards81), "order": order}, timeout)
+
+    def _request(self, peer, msg, timeout):
         tid = next(self._task_ids)
         ev = threading.Event()
         self._tasks[tid] = [ev, None]
         try:
-            self.send(peer, {"type": "solve", "sudoku": sudoku, "task": tid, "address": self.id})
+            msg = dict(msg, task=tid, address=self.id)
+            self.send(peer, msg)
             if not ev.wait(timeout):
                 raise TimeoutError(f"peer {peer} did not answer task {tid}")
             return self._tasks[tid][1]
@@ -325,22 +516,51 @@ class P2PNode:
             self._tasks.pop(tid, None)
 
     # ------------------------------------------------------------- solving
+    def _forward_target(self):
+        if self.forward_threshold is None or self.solver.batcher.pending() < self.forward_threshold:
+            return None
+        with self.lock:
+            peers = list(self.total_peers)
+        if not peers:
+            return None
+        return peers[next(self._rr) % len(peers)]
+
     def peer_sudoku_solve(self, sudoku):
-        """node.py:534-557: solve one board for an HTTP client."""
+        """node.py:534-557: solve one board for an HTTP client -- on this
+        peer's GPUs, or on a peer's when this one is overloaded."""
         board = [row[:] for row in sudoku]
+        peer = self._forward_target()
+        out = None
+        if peer is not None:
+            try:
+                rep = self.request_solve(peer, board, timeout=self.forward_timeout)
+                with self.lock:
+                    self.forwarded += 1
+                if rep.get("solved"):
+                    _copy_into(board, _flat(rep["sudoku"]))
+                    out = board
+                self.broadcast_stats_soon()
+                return out
+            except TimeoutError:
+                logger.warning("peer %s timed out, solving locally", peer)
         out = self.solver.solve_sudoku(board)
-        self.broadcast_stats()
+        self.broadcast_stats_soon()
         return out
 
     def get_stats(self):
-        """node.py:598-620: {"all": {...}, "nodes": [...]}."""
+        """node.py:598-620: {"all": {...}, "nodes": [...]} (plus "solved_by",
+        the per-node solved counts that the totals sum)."""
+        with self.solver.lock:
+            solved, validations = self.solver.solved_puzzles, self.solver.validations
         with self.lock:
-            if self.solver.solved_puzzles:
-                self.stats_solved[self.id] = max(self.stats_solved.get(self.id, 0), self.solver.solved_puzzles)
-            self._merge_node(self.id, self.solver.validations)
+            if solved:
+                self.stats_solved[self.id] = max(self.stats_solved.get(self.id, 0), solved)
+            self._merge_node(self.id, validations)
             self.all_stats["all"]["solved"] = sum(self.stats_solved.values())
             self.all_stats["all"]["validations"] = sum(n["validations"] for n in self.all_stats["nodes"])
-            return json.loads(json.dumps(self.all_stats))
+            out = json.loads(json.dumps(self.all_stats))
+            out["solved_by"] = [{"address": a, "solved": v} for a, v in sorted(self.stats_solved.items())]
+            return out
 
     def network(self):
         with self.lock:
@@ -373,12 +593,14 @@ class P2PNode:
         self.broadcast_stats()
         self.broadcast({"type": "disconnect", "address": self.id})
         self.shutdown_flag = True
+        self.solver.close()
 
 
 class SudokuHTTPServer(BaseHTTPRequestHandler):
     """node.py:661-704: POST /solve, GET /stats, GET /network."""
 
     p2p_node: P2PNode = None  # set by make_http_server
+    protocol_version = "HTTP/1.1"  # keep-alive: load clients reuse connections
 
     def log_message(self, fmt, *args):
         logger.debug(fmt, *args)
@@ -392,11 +614,12 @@ class SudokuHTTPServer(BaseHTTPRequestHandler):
         self.wfile.write(body)
 
     def do_POST(self):
+        n = int(self.headers.get("Content-Length") or 0)
+        data = self.rfile.read(n)
         if self.path != "/solve":
             return self._send_response({"error": "Invalid endpoint"}, 404)
         try:
-            n = int(self.headers["Content-Length"])
-            sudoku = json.loads(self.rfile.read(n).decode("utf-8"))["sudoku"]
+            sudoku = json.loads(data.decode("utf-8"))["sudoku"]
             as_boards(sudoku)  # shape / range validation
         except Exception as e:
             return self._send_response({"error": f"bad request: {e}"}, 400)
@@ -419,7 +642,9 @@ class SudokuHTTPServer(BaseHTTPRequestHandler):
 
 def make_http_server(p2p_node: P2PNode, host: str, port: int) -> ThreadingHTTPServer:
     handler = type("BoundSudokuHTTPServer", (SudokuHTTPServer,), {"p2p_node": p2p_node})
-    return ThreadingHTTPServer((host, port), handler)
+    srv = ThreadingHTTPServer((host, port), handler)
+    srv.daemon_threads = True
+    return srv
 
 
 def main(argv=None):
@@ -430,11 +655,13 @@ def main(argv=None):
     ap.add_argument("-h", type=float, default=1, help="Handicap (delay in ms) for validation")
     ap.add_argument("--host", default="127.0.0.1")
     ap.add_argument("--gpus", default=None, help="comma list of local GPU indices (default: current)")
+    ap.add_argument("--forward-threshold", type=int, default=None,
+                    help="hand new boards to peers while this many wait for the local GPUs")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
     devices = [int(x) for x in args.gpus.split(",")] if args.gpus else None
     node = P2PNode(args.host, args.s, anchor_node=args.a, handicap=args.h / 100,
-                   backend=GpuSolverBackend(devices))
+                   backend=GpuSolverBackend(devices), forward_threshold=args.forward_threshold)
     node.bind()
     httpd = make_http_server(node, args.host, args.p)
     threading.Thread(target=httpd.serve_forever, daemon=True).start()

@@ -10,6 +10,7 @@ Boards are ``uint8`` tensors of shape ``(n, 81)`` (row-major, 0 = empty).
 from __future__ import annotations
 
 import ctypes
+import threading
 from typing import Optional, Tuple
 
 import numpy as np
@@ -67,11 +68,20 @@ def as_boards(x, device=None, max_value: int = 9) -> torch.Tensor:
 
 
 class BatchSolver:
-    """One per device.  Holds the small device workspace of the C ABI."""
+    """One per device.  Holds the device workspace of the C ABI.
+
+    Thread-safe: the workspace is single-stream (include/sudoku_hip.h), so
+    every call that uses it (solve, stats) runs under one lock, and a call on
+    a different stream than the previous one first makes its stream wait for
+    the previous stream's work."""
 
     def __init__(self, device=None):
         self.device = _require_gpu(device)
         self.lib = _lib.load()
+        self._lock = threading.Lock()
+        self._last_stream = None
+        # held by callers that need solve + stats as one step (node.py's backend)
+        self.op_lock = threading.RLock()
         with torch.cuda.device(self.device):
             self.workspace = torch.zeros(int(self.lib.sdk_workspace_bytes()), dtype=torch.uint8,
                                          device=self.device)
@@ -79,6 +89,16 @@ class BatchSolver:
     # ------------------------------------------------------------ helpers
     def _stream(self, stream) -> int:
         s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        return int(s.cuda_stream)
+
+    def _ws_stream(self, stream) -> int:
+        """Stream handle for a workspace call (caller holds self._lock)."""
+        s = stream if stream is not None else torch.cuda.current_stream(self.device)
+        if self._last_stream is not None and self._last_stream != s:
+            ev = torch.cuda.Event()
+            ev.record(self._last_stream)
+            s.wait_event(ev)
+        self._last_stream = s
         return int(s.cuda_stream)
 
     def _dev(self, t: torch.Tensor) -> torch.Tensor:
@@ -102,10 +122,10 @@ class BatchSolver:
             raise ValueError("out must be a contiguous (n, 81) uint8 tensor")
         if status.shape != (n,) or status.dtype != torch.int32:
             raise ValueError("status must be an (n,) int32 tensor")
-        with torch.cuda.device(self.device):
+        with self._lock, torch.cuda.device(self.device):
             rc = self.lib.sdk_solve_batch(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
                                           self.workspace.data_ptr(), _lib.order_code(order),
-                                          1 if ordered else 0, self._stream(stream))
+                                          1 if ordered else 0, self._ws_stream(stream))
         _lib.check(rc, "sdk_solve_batch")
         return out, status
 
@@ -151,8 +171,8 @@ class BatchSolver:
 
     def stats(self, reset: bool = False, stream=None) -> dict:
         out = (ctypes.c_int64 * 6)()
-        with torch.cuda.device(self.device):
-            rc = self.lib.sdk_read_stats(self.workspace.data_ptr(), out, 1 if reset else 0, self._stream(stream))
+        with self._lock, torch.cuda.device(self.device):
+            rc = self.lib.sdk_read_stats(self.workspace.data_ptr(), out, 1 if reset else 0, self._ws_stream(stream))
         _lib.check(rc, "sdk_read_stats")
         return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4],
                 "deferred": out[5]}
@@ -192,11 +212,13 @@ class BatchSolver:
 
 
 _SOLVERS = {}
+_SOLVERS_LOCK = threading.Lock()
 
 
 def get_solver(device=None) -> BatchSolver:
     dev = _require_gpu(device)
-    s = _SOLVERS.get(dev.index)
-    if s is None:
-        s = _SOLVERS[dev.index] = BatchSolver(dev)
-    return s
+    with _SOLVERS_LOCK:
+        s = _SOLVERS.get(dev.index)
+        if s is None:
+            s = _SOLVERS[dev.index] = BatchSolver(dev)
+        return s

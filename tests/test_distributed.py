@@ -1,8 +1,10 @@
-"""Multi-rank orchestration on CPU: world_size 2 over gloo.
+"""Multi-rank orchestration: world_size 2 over gloo.
 
-The per-rank compute is the oracle (test-side backend); the product path
-swaps in GpuBackend (HIP kernels) and RCCL -- same code in
-sudoku_solver_distributed_amd/distributed.py.
+CPU tests: the per-rank compute is the oracle (test-side backend).  The GPU
+test runs the product backend (GpuBackend, HIP kernels) in both ranks, both
+on cuda:0, through the same orchestration code
+(sudoku_solver_distributed_amd/distributed.py); RCCL replaces gloo on a
+multi-GPU node (bench.py --gpus N under torchrun).
 """
 import os
 import socket
@@ -115,3 +117,47 @@ def test_shard_bounds():
             assert spans[0][0] == 0 and spans[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
             assert max(h - l for l, h in spans) - min(h - l for l, h in spans) <= 1
+
+
+def _gpu_worker(rank, world, port, results):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        from sudoku_solver_distributed_amd.distributed import GpuBackend, solve_shard, solve_split
+        from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, hard17_batch
+        be = GpuBackend("cuda:0")
+        batch = hard17_batch(1 << 16, seed=31)
+        (lo, hi), sols, sts = solve_shard(batch, order="gen", backend=be, gather=True)
+        out = {"span": (lo, hi), "sols": sols.cpu().numpy(), "st": sts.cpu().numpy(), "split": {}}
+        board = torch.tensor([[int(c) for c in SEARCH_HEAVY]], dtype=torch.uint8)
+        for order in ("gen", "node"):
+            st = {}
+            ok, grid = solve_split(board, order=order, target=512, chunk=16, backend=be, stats=st)
+            out["split"][order] = (ok, grid.cpu().numpy(), st)
+        results[rank] = out
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_two_rank_gpu_backend():
+    """solve_shard (gather) on 2^16 hard boards and solve_split on a
+    search-heavy board, both ranks on the HIP backend: every rank ends with
+    the oracle's answers (unique completions = the walk's, gen.py:6-28)."""
+    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, hard17_batch
+    mgr = mp.Manager()
+    results = mgr.dict()
+    mp.spawn(_gpu_worker, args=(2, _free_port(), results), nprocs=2, join=True)
+    want, cnt = O.solve_unique_batch(hard17_batch(1 << 16, seed=31).numpy())
+    assert (cnt == 1).all()
+    hw, hc = O.solve_unique_batch(np.array([[int(c) for c in SEARCH_HEAVY]], dtype=np.uint8))
+    for r in range(2):
+        res = results[r]
+        assert res["span"] == (0, 1 << 16)
+        assert (res["st"] == 1).all() and np.array_equal(res["sols"], want)
+        for order in ("gen", "node"):
+            ok, grid, st = res["split"][order]
+            assert ok and np.array_equal(grid, hw[0]), (r, order, st)
+            assert st["frontier"] > 16, st

@@ -378,3 +378,16 @@ def test_stats_agree_between_kernels(solver):
     assert got["packed"]["guesses"] > 20000 * 0.3, got
     assert got["packed"]["guesses"] <= got["plane"]["guesses"] <= got["packed"]["guesses"] * 1.01 + 16, got
     assert got["plane"]["sweeps"] > 20000 * 5, got
+
+
+def test_configs1_full_size(solver):
+    """BASELINE.json configs[1] at its full size: 100k gen.py-generated
+    boards (generate_sudoku(50) x 100k under one seed, gen.py:31-52), solved
+    in one batch and diffed board by board against the literal gen.py:6-28
+    walk (oracle, one walk per host thread)."""
+    from sudoku_solver_distributed_amd.gen import generate_batch
+    puzzles = generate_batch(100_000, 50, seed=7, device=solver.device)
+    sols, st = solver.solve(puzzles)
+    want, wst = O.solve_batch_parallel(puzzles.cpu().numpy(), order="gen", workers=O.host_threads())
+    assert np.array_equal(st.cpu().numpy(), wst)
+    assert np.array_equal(sols.cpu().numpy(), want)

@@ -1,10 +1,13 @@
-"""node.py mirror: HTTP /solve, /stats, /network and the UDP protocol,
-two peers on 127.0.0.1.  CPU tests inject an oracle-backed solver backend
-(test infrastructure); test_node_gpu runs the same flow on the HIP kernels."""
+"""node.py mirror: HTTP /solve, /stats, /network and the UDP protocol on
+127.0.0.1 -- two peers, and a four-peer network under concurrent /solve
+load (BASELINE.json configs[4]).  CPU tests inject an oracle-backed solver
+backend (test infrastructure); the -m gpu tests run the same flows on the
+HIP kernels."""
 import json
 import threading
 import time
 import urllib.request
+from concurrent.futures import ThreadPoolExecutor
 
 import numpy as np
 import pytest
@@ -15,8 +18,11 @@ from oracle import oracle as O
 
 
 class OracleBackend:
+    """node.py's walk exactly (is_valid_move short-circuit included), like
+    the HIP backend."""
+
     def solve(self, boards, order):
-        sols, st = O.solve_batch(boards.numpy(), order=order)
+        sols, st = O.solve_batch(boards.numpy(), order="node_literal" if order == "node" else order)
         return torch.from_numpy(sols), torch.from_numpy(st), 1
 
     def check(self, boards, mode):
@@ -31,9 +37,9 @@ class OracleBackend:
         return torch.tensor(out, dtype=torch.int32)
 
 
-def _start(backend, anchor=None):
+def _start(backend, anchor=None, **kw):
     from sudoku_solver_distributed_amd.node import P2PNode, make_http_server
-    node = P2PNode("127.0.0.1", 0, anchor_node=anchor, handicap=0, backend=backend)
+    node = P2PNode("127.0.0.1", 0, anchor_node=anchor, handicap=0, backend=backend, **kw)
     node.bind()
     httpd = make_http_server(node, "127.0.0.1", 0)
     threading.Thread(target=httpd.serve_forever, daemon=True).start()
@@ -114,3 +120,112 @@ def test_node_requires_gpu_backend_without_gpu():
 def test_node_flow_gpu():
     from sudoku_solver_distributed_amd.node import GpuSolverBackend
     _run_flow(GpuSolverBackend())
+
+
+def _load_boards(n):
+    """n request boards: reference-generated puzzles (golden_gen, 5-58
+    blanks), the README puzzle, short-circuit boards (golden_sc), cycled."""
+    pool = [c["puzzle"] for c in load_golden("golden_gen.json") if 5 <= c["empty_boxes"] <= 58]
+    pool += [c["puzzle"] for c in load_golden("golden_solve.json") if c["name"] == "readme"]
+    pool += [c["puzzle"] for c in load_golden("golden_sc.json")[:8]]
+    return [pool[i % len(pool)] for i in range(n)]
+
+
+def _network(backends, forward=None):
+    """Peers 1..k-1 anchor to peer 0; wait until every peer knows every peer."""
+    nodes = [_start(backends[0], forward_threshold=(forward or {}).get(0))]
+    for i in range(1, len(backends)):
+        nodes.append(_start(backends[i], anchor=nodes[0][0].id, forward_threshold=(forward or {}).get(i)))
+    ids = {n[0].id for n in nodes}
+    for _ in range(200):
+        if all(set(n[0].total_peers) | {n[0].id} == ids for n in nodes):
+            break
+        time.sleep(0.05)
+    assert all(set(n[0].total_peers) | {n[0].id} == ids for n in nodes), [n[0].total_peers for n in nodes]
+    return nodes
+
+
+def _load(nodes, boards, clients=16):
+    """Concurrent POST /solve of every board, spread over the peers' HTTP
+    ports; returns the answers in board order."""
+    def one(i):
+        code, sol = _http(nodes[i % len(nodes)][2] + "/solve", {"sudoku": grid9(boards[i])})
+        return code, sol
+    with ThreadPoolExecutor(max_workers=clients) as ex:
+        return list(ex.map(one, range(len(boards))))
+
+
+def _check_network_run(nodes, boards, answers):
+    want, wst = O.solve_batch(np.array([b81(b) for b in boards], dtype=np.uint8), order="node_literal")
+    for i, ((code, sol), w, ok) in enumerate(zip(answers, want, wst)):
+        if ok:
+            assert code == 200 and [v for r in sol for v in r] == w.tolist(), (i, boards[i])
+        else:
+            assert code == 400, (i, boards[i])
+    solved = int(wst.sum())
+    # gossip converges: every peer's /stats totals count every solved board once
+    for _ in range(200):
+        stats = [_http(n[2] + "/stats")[1] for n in nodes]
+        if all(s["all"]["solved"] == solved for s in stats):
+            break
+        time.sleep(0.05)
+    assert all(s["all"]["solved"] == solved for s in stats), [s["all"] for s in stats]
+    own = {n[0].id: n[0].solver.solved_puzzles for n in nodes}
+    assert sum(own.values()) == solved
+    for s in stats:
+        by = {e["address"]: e["solved"] for e in s["solved_by"]}
+        assert all(by.get(a, 0) == v for a, v in own.items()), (by, own)
+        assert s["all"]["validations"] == sum(e["validations"] for e in s["nodes"])
+    return own
+
+
+def _shutdown(nodes):
+    for n, h, _ in nodes:
+        n.shutdown()
+        h.shutdown()
+
+
+def test_four_peer_network_under_load():
+    """configs[4] on CPU: four peers, 120 concurrent /solve requests spread
+    over their HTTP ports; every answer is node.py's walk (literal oracle),
+    every peer's /stats totals agree, and the batcher coalesced requests."""
+    nodes = _network([OracleBackend() for _ in range(4)])
+    try:
+        boards = _load_boards(120)
+        own = _check_network_run(nodes, boards, _load(nodes, boards))
+        assert all(v > 0 for v in own.values()), own
+        assert sum(n[0].solver.batcher.batches for n in nodes) < len(boards)
+    finally:
+        _shutdown(nodes)
+
+
+def test_four_peer_forwarding():
+    """A peer over its forward threshold hands whole boards to its peers over
+    UDP (solve / solution with a task id): peer 0 forwards every request, the
+    others solve them, and the answers and totals are unchanged."""
+    nodes = _network([OracleBackend() for _ in range(4)], forward={0: 0})
+    try:
+        boards = _load_boards(48)
+        answers = _load(nodes[:1], boards, clients=8)  # every request enters at peer 0
+        own = _check_network_run(nodes, boards, answers)
+        assert nodes[0][0].forwarded == len(boards) and own[nodes[0][0].id] == 0
+        assert sum(n[0].served for n in nodes[1:]) == len(boards)
+    finally:
+        _shutdown(nodes)
+
+
+@pytest.mark.gpu
+def test_two_peer_gpu_network_under_load():
+    """configs[4] on the HIP path: two peers (this box has one MI355X; each
+    peer's GpuSolverBackend shards over the GPUs it is given), 400 concurrent
+    /solve requests, answers bit-identical to node.py's walk, totals agree,
+    and the requests were coalesced into far fewer GPU batches."""
+    from sudoku_solver_distributed_amd.node import GpuSolverBackend
+    nodes = _network([GpuSolverBackend([0]), GpuSolverBackend([0])])
+    try:
+        boards = _load_boards(400)
+        _check_network_run(nodes, boards, _load(nodes, boards, clients=32))
+        batches = sum(n[0].solver.batcher.batches for n in nodes)
+        assert batches < len(boards) // 2, batches
+    finally:
+        _shutdown(nodes)
