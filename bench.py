@@ -27,6 +27,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -62,18 +63,81 @@ def _time(fn, reps=3):
     return best, out
 
 
-def side_configs(solver, dev, world, rank):
-    """BASELINE.json configs[1] and configs[3], outside the timed region.
+def node_load(dev, requests: int = 2000, clients: int = 32):
+    """BASELINE.json configs[4] serving figure: one in-process peer
+    (node.py mirror, GpuSolverBackend on this GPU) answering concurrent HTTP
+    POST /solve from `clients` client threads; requests/s and latency."""
+    import urllib.request
+    from concurrent.futures import ThreadPoolExecutor
+
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    from sudoku_solver_distributed_amd.node import GpuSolverBackend, P2PNode, make_http_server
+    node = P2PNode("127.0.0.1", 0, handicap=0, backend=GpuSolverBackend([dev.index]))
+    node.bind()
+    httpd = make_http_server(node, "127.0.0.1", 0)
+    threading.Thread(target=httpd.serve_forever, daemon=True).start()
+    url = f"http://127.0.0.1:{httpd.server_address[1]}/solve"
+    boards = hard17_batch(requests, seed=77).numpy()
+    bodies = [json.dumps({"sudoku": b.reshape(9, 9).tolist()}).encode() for b in boards]
+
+    def one(i):
+        t0 = time.perf_counter()
+        req = urllib.request.Request(url, data=bodies[i], headers={"Content-Type": "application/json"})
+        with urllib.request.urlopen(req, timeout=60) as r:
+            sol = json.loads(r.read())
+        return time.perf_counter() - t0, sum(sum(row) for row in sol) == 405
+    try:
+        with ThreadPoolExecutor(max_workers=clients) as ex:
+            list(ex.map(one, range(min(64, requests))))  # warm-up
+            b0 = node.solver.batcher.batches
+            t0 = time.perf_counter()
+            res = list(ex.map(one, range(requests)))
+            el = time.perf_counter() - t0
+        lat = sorted(r[0] for r in res)
+        return {"requests": requests, "clients": clients, "requests_per_s": requests / el,
+                "p50_ms": lat[len(lat) // 2] * 1e3, "p99_ms": lat[int(len(lat) * 0.99)] * 1e3,
+                "gpu_batches": node.solver.batcher.batches - b0, "all_solved": all(r[1] for r in res)}
+    finally:
+        node.shutdown()
+        httpd.shutdown()
+
+
+def e2e_rate(solver, boards, reps: int = 3):
+    """PCIe-inclusive rate: pinned host boards in, host solutions and
+    statuses out (the serving path's view); `value` is device-resident."""
+    import torch
+    host = boards.cpu().pin_memory()
+    out_h = torch.empty_like(host).pin_memory()
+    st_h = torch.empty(host.shape[0], dtype=torch.int32).pin_memory()
+
+    def run():
+        d = host.to(solver.device, non_blocking=True)
+        sols, st = solver.solve(d)
+        out_h.copy_(sols, non_blocking=True)
+        st_h.copy_(st, non_blocking=True)
+        return st_h
+    t, st = _time(run, reps)
+    return {"boards": host.shape[0], "ms": t * 1e3, "boards_per_s": host.shape[0] / t,
+            "all_solved": bool((st == 1).all())}
+
+
+def side_configs(solver, dev, world, rank, boards):
+    """BASELINE.json configs[1], [3] and [4], a search-heavy batch and the
+    PCIe-inclusive rate, outside the timed region.
 
     configs[1]: 100k gen.py-style boards (generate_sudoku(50) under one seed,
     same random calls as gen.py:31-52) solved in one batch on one GPU.
     configs[3]: one search-heavy board, the walk's direct single-wave solve
     vs the frontier split (over every rank's GPU when N > 1, RCCL
-    all-reduce(MIN) early-exit word).  Every result is checked.
+    all-reduce(MIN) early-exit word).
+    configs[4]: concurrent HTTP /solve against one peer (node_load).
+    hard_search: 2^20 boards that need real search (gen.hard_search_batch).
+    e2e: the timed batch with host buffers on both sides.
+    Every result is checked.
     """
     import torch
     from sudoku_solver_distributed_amd.distributed import solve_split
-    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, generate_batch
+    from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, generate_batch, hard_search_batch
     out = {}
     if rank == 0:
         gen = generate_batch(100_000, 50, seed=7, device=dev)
@@ -81,6 +145,18 @@ def side_configs(solver, dev, world, rank):
         ok = bool((st == 1).all()) and bool((solver.check(sols, 0) == 1).all())
         out["gen100k"] = {"boards": 100_000, "empty_boxes": 50, "seconds": t, "boards_per_s": 100_000 / t,
                           "all_solved_and_checked": ok}
+        hs = hard_search_batch(boards.shape[0], seed=5, device=dev)
+        solver.solve(hs)
+        solver.stats(reset=True)
+        t, (sols, st) = _time(lambda: solver.solve(hs))
+        s3 = solver.stats(reset=True)
+        ok = bool((st == 1).all()) and bool((solver.check(sols, 0) == 1).all())
+        out["hard_search"] = {"boards": hs.shape[0], "seconds": t, "boards_per_s": hs.shape[0] / t,
+                              "guesses_per_board": s3["guesses"] / max(s3["finished"], 1),
+                              "passes_per_board": s3["sweeps"] / max(s3["finished"], 1),
+                              "deferred_per_call": s3["deferred"] / 3, "all_solved_and_checked": ok}
+        out["e2e"] = e2e_rate(solver, boards)
+        out["node_http"] = node_load(dev)
     board = torch.tensor([[int(c) for c in SEARCH_HEAVY]], dtype=torch.uint8, device=dev)
     t_direct, (g1, s1) = _time(lambda: solver.solve(board))
     st = {}
@@ -171,7 +247,7 @@ def main():
     lat.sort()
     p50 = lat[len(lat) // 2] if lat else None
 
-    extras = None if args.no_extras else side_configs(solver, dev, world, rank)
+    extras = None if args.no_extras else side_configs(solver, dev, world, rank, boards)
 
     if rank != 0:
         if world > 1:

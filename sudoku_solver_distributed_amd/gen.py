@@ -12,9 +12,12 @@
   a unique solution, made by validity-preserving symmetries (digit relabeling,
   row/column permutations inside bands/stacks, band/stack permutations,
   transposition) of seed boards certified unique.
+* ``hard_search_batch(n, seed)`` -- the search-heavy set: the same symmetries
+  applied to 256 minimal puzzles that need real search (data/).
 """
 from __future__ import annotations
 
+import os
 import random as _random
 import sys
 from typing import List, Optional
@@ -132,11 +135,14 @@ def _perms(rng: np.random.Generator, shape, k: int) -> np.ndarray:
     return np.argsort(rng.random(tuple(shape) + (k,)), axis=-1)
 
 
-def hard17_batch(n: int, seed: int = 0, seeds=SEEDS_17, device=None) -> torch.Tensor:
-    """n 17-clue unique-solution boards (symmetry images of `seeds`), as a
-    (n, 81) uint8 tensor on `device` (host if device is None)."""
+def _symmetry_images(base: np.ndarray, n: int, seed: int) -> np.ndarray:
+    """n random validity-preserving images of the (k, 81) boards `base`:
+    digit relabeling, row / column permutations inside bands / stacks,
+    band / stack permutations, transposition.  Clue count, number of
+    completions and logical difficulty are invariants; the walk's cell
+    order sees a different board each time."""
     rng = np.random.default_rng(seed)
-    base = np.array([[int(c) for c in s] for s in seeds], dtype=np.uint8).reshape(-1, 9, 9)
+    base = base.reshape(-1, 9, 9)
     which = rng.integers(len(base), size=n)
     relabel = np.zeros((n, 10), dtype=np.uint8)
     relabel[:, 1:] = _perms(rng, (n,), 9) + 1
@@ -147,8 +153,33 @@ def hard17_batch(n: int, seed: int = 0, seeds=SEEDS_17, device=None) -> torch.Te
     b = np.where(trans[:, None, None], b.transpose(0, 2, 1), b)
     b = np.take_along_axis(b, np.repeat(rows[:, :, None], 9, axis=2), axis=1)
     b = np.take_along_axis(b, np.repeat(cols[:, None, :], 9, axis=1), axis=2)
-    out = np.take_along_axis(relabel, b.reshape(n, 81).astype(np.int64), axis=1).astype(np.uint8)
-    t = torch.from_numpy(np.ascontiguousarray(out))
+    return np.take_along_axis(relabel, b.reshape(n, 81).astype(np.int64), axis=1).astype(np.uint8)
+
+
+def hard17_batch(n: int, seed: int = 0, seeds=SEEDS_17, device=None) -> torch.Tensor:
+    """n 17-clue unique-solution boards (symmetry images of `seeds`), as a
+    (n, 81) uint8 tensor on `device` (host if device is None)."""
+    base = np.array([[int(c) for c in s] for s in seeds], dtype=np.uint8)
+    t = torch.from_numpy(np.ascontiguousarray(_symmetry_images(base, n, seed)))
+    return t.to(device) if device is not None else t
+
+
+_HARD_SEARCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "hard_search_seeds.txt")
+
+
+def hard_search_seeds() -> List[str]:
+    """The search-heavy seed boards (data/hard_search_seeds.txt, made by
+    scripts/make_hard_search.py): minimal unique puzzles from gen.py-style
+    grids that naked + hidden singles cannot finish (>= 2 guesses)."""
+    with open(_HARD_SEARCH) as f:
+        return [ln.split()[0] for ln in f if ln.strip() and not ln.startswith("#")]
+
+
+def hard_search_batch(n: int, seed: int = 0, device=None) -> torch.Tensor:
+    """n search-heavy unique-solution boards (symmetry images of
+    hard_search_seeds()), as a (n, 81) uint8 tensor."""
+    base = np.array([[int(c) for c in s] for s in hard_search_seeds()], dtype=np.uint8)
+    t = torch.from_numpy(np.ascontiguousarray(_symmetry_images(base, n, seed)))
     return t.to(device) if device is not None else t
 
 

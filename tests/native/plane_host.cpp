@@ -87,3 +87,32 @@ extern "C" int64_t plane_check_load(const uint8_t *in, int64_t n)
     }
     return bad;
 }
+
+// per-board passes / guesses / deepest stack level of the plane solver
+// (scripts/make_hard_search.py filters search-heavy boards with it)
+struct DepthStack {
+    HostStack s;
+    uint32_t max_depth = 0;
+    void put(uint32_t d, int k, uint32_t v) { s.put(d, k, v); if (d + 1 > max_depth) max_depth = d + 1; }
+    uint32_t get(uint32_t d, int k) const { return s.get(d, k); }
+};
+
+extern "C" void plane_solve_stats(const uint8_t *in, int64_t n, int node_order, int32_t *passes, int32_t *guesses,
+                                  int32_t *depth)
+{
+    static DepthStack stk;
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t x[21];
+        words_of(in + i * 81, x);
+        plane::Board B;
+        bool clash = false;
+        passes[i] = guesses[i] = depth[i] = -1;
+        if (!plane::load_words(B, x, clash) || clash) continue;
+        plane::Stats st = {0, 0};
+        stk.max_depth = 0;
+        plane::solve(B, stk, node_order, 81, st);
+        passes[i] = (int32_t)st.passes;
+        guesses[i] = (int32_t)st.guesses;
+        depth[i] = (int32_t)stk.max_depth;
+    }
+}

@@ -391,3 +391,38 @@ def test_configs1_full_size(solver):
     want, wst = O.solve_batch_parallel(puzzles.cpu().numpy(), order="gen", workers=O.host_threads())
     assert np.array_equal(st.cpu().numpy(), wst)
     assert np.array_equal(sols.cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_hard_search_vs_unique_oracle(solver, order):
+    """The search-heavy set (minimal puzzles that need ~10 guesses): unique
+    completions, so every walk's answer is the oracle's completion."""
+    from sudoku_solver_distributed_amd.gen import hard_search_batch
+    p = hard_search_batch(4096, seed=21)
+    sols, st = solver.solve(p, order=order)
+    want, cnt = O.solve_unique_batch(p.numpy())
+    assert (cnt == 1).all()
+    assert (st.cpu().numpy() == 1).all()
+    assert np.array_equal(sols.cpu().numpy(), want)
+
+
+def test_hard_search_4m(solver):
+    """4M search-heavy boards in one call: every board solved (status and the
+    GPU Sudoku.check), givens kept, 256 sampled boards equal to the oracle,
+    and no board handed to the wave kernel for depth (the stack holds 32
+    levels; this set needs <= 13)."""
+    from sudoku_solver_distributed_amd.gen import hard_search_batch
+    n = 1 << 22
+    p = hard_search_batch(n, seed=2025, device=solver.device)
+    solver.stats(reset=True)
+    sols, st = solver.solve(p)
+    stats = solver.stats(reset=True)
+    assert bool((st == 1).all())
+    assert bool((solver.check(sols, 0) == 1).all())
+    givens = p != 0
+    assert bool((sols[givens] == p[givens]).all())
+    assert stats["finished"] == n and stats["deferred"] == 0, stats
+    assert stats["guesses"] > 5 * n, stats
+    idx = torch.randint(0, n, (256,), generator=torch.Generator().manual_seed(2))
+    want, cnt = O.solve_unique_batch(p[idx.to(p.device)].cpu().numpy())
+    assert np.array_equal(sols[idx.to(p.device)].cpu().numpy(), want)
