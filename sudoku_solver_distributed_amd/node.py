@@ -640,11 +640,14 @@ class SudokuHTTPServer(BaseHTTPRequestHandler):
             self._send_response({"error": "Invalid endpoint"}, 404)
 
 
+class _Server(ThreadingHTTPServer):
+    daemon_threads = True
+    request_queue_size = 1024  # socketserver's default listen backlog (5) resets concurrent clients
+
+
 def make_http_server(p2p_node: P2PNode, host: str, port: int) -> ThreadingHTTPServer:
     handler = type("BoundSudokuHTTPServer", (SudokuHTTPServer,), {"p2p_node": p2p_node})
-    srv = ThreadingHTTPServer((host, port), handler)
-    srv.daemon_threads = True
-    return srv
+    return _Server((host, port), handler)
 
 
 def main(argv=None):

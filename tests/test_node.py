@@ -145,7 +145,7 @@ def _network(backends, forward=None):
     return nodes
 
 
-def _load(nodes, boards, clients=16):
+def _load(nodes, boards, clients=32):
     """Concurrent POST /solve of every board, spread over the peers' HTTP
     ports; returns the answers in board order."""
     def one(i):
