@@ -48,6 +48,10 @@ def main():
            "hbm_bytes_per_launch": None}
     if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
         res["hbm_bytes_per_launch"] = (2 * summary["FETCH_SIZE"] + summary["WRITE_SIZE"]) * 1024
+    if "SQ_WAVE_CYCLES" in summary:
+        for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
+            if k in summary:
+                res[k.lower() + "_share"] = summary[k] / summary["SQ_WAVE_CYCLES"]
     with open(out, "w") as f:
         json.dump(res, f, indent=1)
     print(json.dumps(res, indent=1))

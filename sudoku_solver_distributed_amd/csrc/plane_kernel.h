@@ -146,6 +146,41 @@ __device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, u
     st[2] = sweeps;
 }
 
+// ---- cooperative span loads through LDS
+// A refill (and the start-up) takes k <= 64 CONSECUTIVE boards from the
+// queue, i.e. one contiguous byte span of the batch.  It lands in the wave's
+// LDS staging area by buffer_load_dword ... lds (one wave instruction per 64
+// dwords, all in flight together, no VGPRs), so a refill costs one HBM round
+// trip instead of one per board; the per-board ballots then read bytes from
+// LDS.  Bytes past the batch read as 0 (buffer range check).
+enum { PLANE_STAGE_DWORDS = 1344 };  // >= (3 + 64*81 + 3) / 4, rounded up to 64
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+__device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__ puzzles, int64_t n, int64_t q0, int k,
+                                                     uint32_t *stage, int lane)
+{
+    const uint64_t start = (uint64_t)q0 * 81u, a0 = start & ~3ull, total = (uint64_t)n * 81u;
+    const uint32_t shift = (uint32_t)(start - a0);
+    const uint64_t avail = total - a0;
+    const uint32_t nrec = avail > 0xFFFFFFF0ull ? 0xFFFFFFF0u : (uint32_t)avail;
+    const __amdgpu_buffer_rsrc_t rsrc =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(puzzles + a0), 0, (int)nrec, 0x00020000);
+    const uint32_t nd = (shift + 81u * (uint32_t)k + 3u) / 4u;
+    for (uint32_t i = 0; i < nd; i += 64)
+        __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t *)(stage + i), 4, (int)((i + lane) * 4u), 0, 0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // the batch's last dword may be partial: the range check zeroes all of
+    // it, so its bytes come in one by one
+    const uint64_t tail = total & ~3ull;
+    if ((total & 3u) && tail >= a0 && tail < a0 + 4ull * nd) {
+        uint8_t *sb = (uint8_t *)stage;
+        if ((uint64_t)lane < (total & 3u)) sb[tail - a0 + lane] = puzzles[tail + lane];
+        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    return shift;
+}
+
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -171,6 +206,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     int order, int refill, int tail)
 {
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
+    __shared__ uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
+    uint32_t *stage = stage_lds[threadIdx.x >> 6];
+    const uint8_t *stage_b = (const uint8_t *)stage;
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
     const PlaneStack stk = {
@@ -196,23 +234,25 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     uint32_t st_after = 0;
 #endif
 
-    // Start-up: every lane loads its own first board, all lanes and all 81
-    // byte loads at once.  The cooperative refill below loads one board per
-    // HBM round trip, which for a wave's first 64 boards is ~10 passes' time.
+    // Start-up: the wave's first 64 boards arrive as one staged span; each
+    // lane then converts its own board (plane::load_words), all lanes at once.
     {
         unsigned long long base = 0;
         if (lane == 0) base = atomicAdd(&ws[WS_QUEUE], 64ull);
         base = rdlane64(base, 0);
         drained = (int64_t)base + 64 >= n;
         const int64_t q = (int64_t)base + lane;
+        const int64_t kk = (int64_t)base < n ? (n - (int64_t)base < 64 ? n - (int64_t)base : 64) : 0;
+        const uint32_t sh = kk ? plane_stage_span(puzzles, n, (int64_t)base, (int)kk, stage, lane) : 0u;
         if (q < n) {
             fin++;
             const uint8_t *src = puzzles + q * 81;
+            const uint8_t *sb = stage_b + sh + 81u * (uint32_t)lane;
             uint32_t x[21];
 #pragma unroll
             for (int k = 0; k < 21; ++k) {
-                uint32_t w = src[4 * k];
-                if (k < 20) w |= ((uint32_t)src[4 * k + 1] << 8) | ((uint32_t)src[4 * k + 2] << 16) | ((uint32_t)src[4 * k + 3] << 24);
+                uint32_t w = sb[4 * k];
+                if (k < 20) w |= ((uint32_t)sb[4 * k + 1] << 8) | ((uint32_t)sb[4 * k + 2] << 16) | ((uint32_t)sb[4 * k + 3] << 24);
                 x[k] = w;
             }
             bool clash;  // tested lazily (see the unsolvable store above)
@@ -306,14 +346,17 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 base = __shfl(base, leader);
                 drained = (int64_t)base + k >= n;
                 bool loaded = false;
+                const int kk = (int64_t)base < n ? (int)(n - (int64_t)base < k ? n - (int64_t)base : k) : 0;
+                const uint32_t sh = kk ? plane_stage_span(puzzles, n, (int64_t)base, kk, stage, lane) : 0u;
                 m = idle;
                 for (int64_t q = (int64_t)base; m && q < n; ++q) {
                     const int i = __builtin_ctzll(m);
                     m &= m - 1;
                     if (lane == i) fin++;
                     const uint8_t *src = puzzles + q * 81;
+                    const uint8_t *sb = stage_b + sh + 81u * (uint32_t)(q - (int64_t)base);
                     // slots holding no cell read the sentinel 0x100 (no byte value)
-                    const uint32_t a0 = c0 >= 0 ? src[c0] : 0x100u, a1 = c1 >= 0 ? src[c1] : 0x100u;
+                    const uint32_t a0 = c0 >= 0 ? sb[c0] : 0x100u, a1 = c1 >= 0 ? sb[c1] : 0x100u;
                     if (__builtin_amdgcn_ballot_w64((a0 > 9 && a0 != 0x100u) || (a1 > 9 && a1 != 0x100u))) {
                         plane_copy_board(src, sols + q * 81, lane);  // raw input back
                         if (lane == 0) status[q] = SDK_INVALID;
