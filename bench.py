@@ -276,7 +276,21 @@ def main():
             roof["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]
             if pmc.get("hbm_bytes_per_launch") is not None:
                 roof["traffic"] = pmc["hbm_bytes_per_launch"]
+                roof["traffic_over_algorithmic"] = pmc["hbm_bytes_per_launch"] / (BYTES_PER_BOARD * args.batch)
+            for k in ("sq_wait_inst_any_share", "sq_wait_any_share"):
+                if k in pmc:
+                    roof[k] = pmc[k]
             roof["pmc_source"] = os.path.relpath(PMC_FILE, ROOT)
+            # lanes doing pass work: passes x VALU per pass (ISA count of
+            # plane::pass) over every lane slot the kernel issued
+            isa = os.path.join(PMC_DIR, "isa_plane_pass.json")
+            if kname == "plane_kernel" and os.path.exists(isa):
+                with open(isa) as f:
+                    vpp = json.load(f)["valu_per_pass"]
+                useful = st["sweeps"] / args.steps * vpp
+                roof["valu_per_pass"] = vpp
+                roof["useful_lane_frac"] = useful / ops
+                roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
 
     cpu = None
     if world == 1 and not args.no_cpu:
