@@ -175,6 +175,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=1 << 20, help="boards per GPU per step")
     ap.add_argument("--seed", type=int, default=2024)
+    ap.add_argument("--workload", choices=("hard17", "hard_search"), default="hard17",
+                    help="timed boards: BASELINE's hard 17-clue set (default, the metric's config) or the "
+                         "search-heavy set (profiling / A/B only)")
     ap.add_argument("--cpu-budget", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-boards", type=int, default=32,
@@ -196,12 +199,13 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    from sudoku_solver_distributed_amd.gen import hard17_batch
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
     from sudoku_solver_distributed_amd.solver import get_solver
 
     solver = get_solver(dev)
     # rank-local shard of synthetic hard boards (weak scaling: B per GPU)
-    boards = hard17_batch(args.batch, seed=args.seed + rank, device=dev)
+    make = hard17_batch if args.workload == "hard17" else hard_search_batch
+    boards = make(args.batch, seed=args.seed + rank, device=dev)
     out = torch.empty_like(boards)
     status = torch.empty(args.batch, dtype=torch.int32, device=dev)
     stream = torch.cuda.current_stream(dev)
@@ -269,7 +273,8 @@ def main():
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if pmc.get("batch") == args.batch and pmc.get("seed") == args.seed and pmc.get("kernel") == kname:
+        if (pmc.get("batch") == args.batch and pmc.get("seed") == args.seed and pmc.get("kernel") == kname
+                and pmc.get("workload", "hard17") == args.workload):
             ops = pmc["valu_insts_per_launch"] * 64
             roof["achieved"] = ops / kern_s / 1e12
             roof["frac"] = roof["achieved"] / roof["peak"]
@@ -314,7 +319,9 @@ def main():
         "vs_baseline": None,
         "dtype": "u8",
         "data": "synthetic: 17-clue unique-solution boards (symmetry images of certified seeds)",
-        "config": {"workload": f"hard 17-clue 9x9 batch, {args.batch} boards per GPU per step",
+        "config": {"workload": (f"hard 17-clue 9x9 batch, {args.batch} boards per GPU per step"
+                                if args.workload == "hard17" else
+                                f"search-heavy minimal 9x9 batch, {args.batch} boards per GPU per step"),
                    "global_batch": args.batch * world, "parallelism": f"shard{world}"},
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,

@@ -17,7 +17,10 @@ SRC = os.path.join(ROOT, "sudoku_solver_distributed_amd", "csrc", "plane_kernels
 
 def main():
     asm = os.path.join(tempfile.mkdtemp(), "plane.s")
-    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC",
+    sys.path.insert(0, ROOT)
+    from sudoku_solver_distributed_amd import build as B  # same flags as the product build
+    extra = dict(B.SRCS)["plane_kernels.hip"]
+    subprocess.check_call(["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", *extra,
                            "--cuda-device-only", "-S", "-o", asm, SRC], stderr=subprocess.DEVNULL)
     lines = open(asm).read().split("\n")
     st = next(i for i, l in enumerate(lines) if l.startswith("_Z12plane_kernel"))
@@ -35,7 +38,7 @@ def main():
     body = max(blocks, key=len)
     c = collections.Counter(body)
     valu = sum(v for k, v in c.items() if k.startswith("v_"))
-    out = {"kernel": "plane_kernel", "source": "plane_kernels.hip (hipcc -O3 gfx950)",
+    out = {"kernel": "plane_kernel", "source": "plane_kernels.hip (hipcc -O3 gfx950 %s)" % " ".join(extra),
            "pass_block_instructions": len(body), "valu_per_pass": valu,
            "salu_per_pass": sum(v for k, v in c.items() if k.startswith("s_")),
            "top": c.most_common(8)}

@@ -79,7 +79,7 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
 int sdk_plane_blocks_per_cu();
 #define PLANE_MAX_DEPTH 32
 #define PLANE_THREADS 256
-#define PLANE_STACK_WORDS 28
+#define PLANE_STACK_WORDS 32  // per level: 27 planes + branch entry, padded to one 128-byte line
 // board indices the plane kernel hands to the wave kernel (int64 each; more
 // than this and the wave kernel finds them by scanning the statuses)
 #define PLANE_DEFER_CAP (1 << 20)

@@ -47,27 +47,66 @@
 #ifndef SDK_PLANE_STAMPS
 #define SDK_PLANE_STAMPS 0
 #endif
-static_assert(PLANE_STACK_WORDS == plane::STACK_WORDS, "stack layout");
+static_assert(plane::STACK_ENTRY == 27, "stack layout");
+typedef uint32_t sdk_v4u __attribute__((ext_vector_type(4)));
 
-// Per-lane stack in the workspace: word w of level L of lane g lives at
-// dword (L*28 + w)*nt + g.  Buffer stores/loads: the lane part of the offset
-// is one VGPR (voffset), the word part is wave-uniform (soffset), so the 28
-// word addresses never become 28 hoisted 64-bit VGPR pairs.
+// Per-lane DFS stack in the workspace: level L of lane g is one 128-byte
+// line at byte (g * PLANE_MAX_DEPTH + L) * 128, words 0..26 = the 27 planes
+// (word 3d+b = P[d][b]), word 27 = the branch entry, 28..31 unused.  A push
+// or pop is 7 buffer dwordx4 accesses to ONE line (guesses are lane-
+// divergent: a lane-interleaved layout made every push touch 28 lines).
 struct PlaneStack {
     __amdgpu_buffer_rsrc_t rsrc;
-    uint32_t lane_off;  // g * 4
-    uint32_t nt4;       // nt * 4: bytes per (level, word) row
-    __device__ __forceinline__ uint32_t voff(uint32_t level) const
+    uint32_t lane_off;  // g * PLANE_MAX_DEPTH * 128
+    __device__ __forceinline__ uint32_t voff(uint32_t level) const { return lane_off + level * 128u; }
+    // a value the optimizer cannot trace back to the board's memory layout:
+    // four consecutive board words gathered into a vector are otherwise
+    // turned into one vector load, which keeps the whole board in scratch
+    static __device__ __forceinline__ uint32_t opaque(uint32_t x)
     {
-        return lane_off + level * (uint32_t)plane::STACK_WORDS * nt4;
+        asm("" : "+v"(x));
+        return x;
     }
-    __device__ __forceinline__ void put(uint32_t level, int w, uint32_t v) const
+    __device__ __forceinline__ void push(uint32_t level, const plane::Board &B, uint32_t entry) const
     {
-        __builtin_amdgcn_raw_buffer_store_b32(v, rsrc, (int)voff(level), (int)((uint32_t)w * nt4), 0);
+        const int v = (int)voff(level);
+#define PQ(a, b, c, d) (sdk_v4u){opaque(B.P[a / 3][a % 3]), opaque(B.P[b / 3][b % 3]), opaque(B.P[c / 3][c % 3]), \
+                                 opaque(B.P[d / 3][d % 3])}
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(0, 1, 2, 3), rsrc, v, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(4, 5, 6, 7), rsrc, v, 16, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(8, 9, 10, 11), rsrc, v, 32, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(12, 13, 14, 15), rsrc, v, 48, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(16, 17, 18, 19), rsrc, v, 64, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(PQ(20, 21, 22, 23), rsrc, v, 80, 0);
+#undef PQ
+        __builtin_amdgcn_raw_buffer_store_b128(
+            (sdk_v4u){opaque(B.P[8][0]), opaque(B.P[8][1]), opaque(B.P[8][2]), entry}, rsrc, v, 96, 0);
     }
-    __device__ __forceinline__ uint32_t get(uint32_t level, int w) const
+    // the last quad: planes 24..26 and the branch entry
+    __device__ __forceinline__ sdk_v4u top(uint32_t level) const
     {
-        return __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)voff(level), (int)((uint32_t)w * nt4), 0);
+        return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff(level), 96, 0);
+    }
+    __device__ __forceinline__ void restore(uint32_t level, plane::Board &B, const sdk_v4u &t) const
+    {
+        const int v = (int)voff(level);
+        const sdk_v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 0, 0);
+        const sdk_v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 16, 0);
+        const sdk_v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 32, 0);
+        const sdk_v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 48, 0);
+        const sdk_v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 64, 0);
+        const sdk_v4u q5 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 80, 0);
+        B.P[0][0] = q0.x; B.P[0][1] = q0.y; B.P[0][2] = q0.z; B.P[1][0] = q0.w;
+        B.P[1][1] = q1.x; B.P[1][2] = q1.y; B.P[2][0] = q1.z; B.P[2][1] = q1.w;
+        B.P[2][2] = q2.x; B.P[3][0] = q2.y; B.P[3][1] = q2.z; B.P[3][2] = q2.w;
+        B.P[4][0] = q3.x; B.P[4][1] = q3.y; B.P[4][2] = q3.z; B.P[5][0] = q3.w;
+        B.P[5][1] = q4.x; B.P[5][2] = q4.y; B.P[6][0] = q4.z; B.P[6][1] = q4.w;
+        B.P[6][2] = q5.x; B.P[7][0] = q5.y; B.P[7][1] = q5.z; B.P[7][2] = q5.w;
+        B.P[8][0] = t.x; B.P[8][1] = t.y; B.P[8][2] = t.z;
+    }
+    __device__ __forceinline__ void put_entry(uint32_t level, uint32_t entry) const
+    {
+        __builtin_amdgcn_raw_buffer_store_b32(entry, rsrc, (int)voff(level), 108, 0);
     }
 };
 
@@ -212,8 +251,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
     const PlaneStack stk = {
-        __builtin_amdgcn_make_buffer_rsrc(stack, 0, (int)(nt * 4 * plane::STACK_WORDS * PLANE_MAX_DEPTH), 0x00020000),
-        (uint32_t)g * 4u, (uint32_t)nt * 4u};
+        __builtin_amdgcn_make_buffer_rsrc(stack, 0, (int)(nt * PLANE_MAX_DEPTH * 128), 0x00020000),
+        (uint32_t)g * (uint32_t)(PLANE_MAX_DEPTH * 128)};
     const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
     const int node_order = order == SDK_ORDER_NODE;
     const int lane = threadIdx.x & 63;
@@ -428,9 +467,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 plane::pick_cell(und, node_order, band, pos);
                 const uint32_t cand = plane::cell_cand(B, band, pos);
                 const uint32_t d = cand & (0u - cand);
-#pragma unroll
-                for (int w = 0; w < 27; ++w) stk.put(depth, w, B.P[w / 3][w % 3]);
-                stk.put(depth, plane::STACK_ENTRY, plane::make_entry(band, pos, cand ^ d));
+                stk.push(depth, B, plane::make_entry(band, pos, cand ^ d));
                 depth++;
                 guesses++;
                 bguess++;
@@ -444,14 +481,14 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     break;
                 }
                 depth--;
-                const uint32_t e = stk.get(depth, plane::STACK_ENTRY);
+                const sdk_v4u t = stk.top(depth);
+                const uint32_t e = t[3];
                 const uint32_t rem = (e >> 8) & 0x1FFu;
                 if (!rem) continue;
                 const uint32_t d = rem & (0u - rem);
-#pragma unroll
-                for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = stk.get(depth, w);
+                stk.restore(depth, B, t);
                 B.Det[0] = B.Det[1] = B.Det[2] = 0;
-                stk.put(depth, plane::STACK_ENTRY, e & ~(d << 8));
+                stk.put_entry(depth, e & ~(d << 8));
                 depth++;
                 guesses++;
                 bguess++;
