@@ -38,7 +38,8 @@ extern "C" {
 
 /* Bytes of device workspace sdk_solve_batch needs on the current device:
  * queue heads, cancel word, statistics, and the plane kernel's per-lane DFS
- * stacks (about 0.94 GB on an MI355X).  Allocate once per device, zero once;
+ * stacks and the deferred-board list (about 1.08 GB on an MI355X).  Allocate
+ * once per device, zero once;
  * the library re-arms the per-call words itself on `stream`.
  * A workspace is SINGLE-STREAM: every call that passes the same workspace
  * must be issued on the same stream (or ordered by the caller), because each
