@@ -30,6 +30,7 @@ extern "C" {
 #define SDK_INVALID -1    /* a byte > 9 in the input (rejected, output = input) */
 #define SDK_CANCELLED -2  /* ordered mode: a lower-indexed board already solved */
 #define SDK_FAULT -3      /* internal consistency check failed (never expected) */
+#define SDK_NO_RETURN -4  /* sdk_peer_solve_batch: node.py's /solve loop never returns */
 
 /* the reference's two walks (cell choice; digits are always tried 1..9) */
 #define SDK_ORDER_GEN 0   /* gen.py:6-28: first empty cell of the LAST row that
@@ -72,6 +73,18 @@ int sdk_check_batch(const uint8_t *d_grids, int32_t *d_ok, int64_t n, int mode, 
  * board i, or 0 for None. */
 int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
                               int32_t *d_num, int64_t n, void *stream);
+
+/* The reference's HTTP /solve algorithm, node.py:534-557
+ * P2PNode.peer_sudoku_solve on a fresh single node (handicap 0, no peers):
+ * a greedy row-major cell loop with node.py's repair step (node.py:419-532),
+ * not a search.  d_out[i] = the board it leaves (valid or not), d_status[i] =
+ * SDK_SOLVED (its final check passed), SDK_UNSOLVABLE (returned, check
+ * failed), SDK_NO_RETURN (node.py loops forever on this board; d_out = the
+ * board at that point) or SDK_INVALID (a byte > 9); d_validations[i] =
+ * node.py's `validations` counter after the call (one per
+ * SudokuSolver.check: every is_valid_move plus the final check). */
+int sdk_peer_solve_batch(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_status, int32_t *d_validations,
+                         int64_t n, void *stream);
 
 /* One level of the reference walk's search tree, for splitting a single hard
  * board over waves / GPUs (node.py's per-cell peer task split, node.py:419-449,

@@ -396,3 +396,104 @@ int64_t oracle_solve_batch_timed(const uint8_t *in, uint8_t *out, int32_t *statu
     }
     return done;
 }
+
+/* ------------------------------------------------------------------------
+ * node.py:534-557 P2PNode.peer_sudoku_solve on a FRESH single node (no
+ * peers, handicap 0): the reference's HTTP /solve path.
+ *   fill_task_queue (node.py:419-425): the empty cells, row-major;
+ *   solve_sudoku (node.py:427-475): pop a cell, take the first digit that
+ *     is_valid_move accepts (solve_sudoku_destributed, node.py:76-80; with
+ *     no peers it runs locally, node.py:443-449), validate_solution;
+ *   validate_solution (node.py:477-532): place the digit, or repair the cell
+ *     by moving a digit placed elsewhere in its row (partial_solution /
+ *     tried_numbers_by_position bookkeeping), or leave it empty (flag False);
+ *   the outer `while True` (node.py:429-464) ends when flag is False, or when
+ *     fewer than 2 cells are empty; otherwise it spins forever.
+ * Returns 1 (final check() passed), 0 (board returned, check failed) or -1
+ * (the reference never returns); *validations = node.py's counter: one per
+ * SudokuSolver.check call (every is_valid_move, plus the final check).
+ * ------------------------------------------------------------------------ */
+static int g_val;
+
+static int peer_valid_move(const uint8_t *g, int row, int col, int num)
+{
+    g_val++;  /* is_valid_move -> self.check(board) (node.py:44, 87) */
+    return oracle_is_valid_move(g, row, col, num);
+}
+
+int oracle_peer_solve(uint8_t *sudoku, int32_t *validations)
+{
+    uint8_t initial[81], partial[81]; /* partial[cell] = digit, 0 = absent */
+    uint8_t tried[81][81];            /* tried[(row,col)][c*9 + v-1]: (row, c, v) tried; row is implied */
+    int queue[1024], qh = 512, qt = 512; /* deque: popleft at qh, append at qt, appendleft at --qh */
+    int flag = 1;
+    memcpy(initial, sudoku, 81);
+    memset(partial, 0, sizeof partial);
+    memset(tried, 0, sizeof tried);
+    g_val = 0;
+    for (int i = 0; i < 81; i++)
+        if (sudoku[i] == 0) queue[qt++] = i;
+    for (;;) {
+        while (qt > qh) {
+            const int cell = queue[qh++], i = cell / 9, j = cell % 9;
+            int num = 0;
+            for (int d = 1; d <= 9 && !num; d++)
+                if (peer_valid_move(sudoku, i, j, d)) num = d;
+            if (num) {                       /* node.py:479-485 */
+                if (peer_valid_move(sudoku, i, j, num)) {
+                    sudoku[cell] = (uint8_t)num;
+                    partial[cell] = (uint8_t)num;
+                } else {
+                    queue[--qh] = cell;
+                }
+                continue;
+            }
+            /* node.py:487-532: repair */
+            flag = 1;
+            uint8_t temp[81];
+            memcpy(temp, sudoku, 81);
+            int vn_cell[9], vn_val[9], nv = 0;
+            for (int c = 0; c < 9; c++) {
+                const int rc = i * 9 + c;
+                if (c == j || !partial[rc]) continue;
+                temp[rc] = 0;
+                const int v = partial[rc];
+                if (peer_valid_move(temp, i, j, v))
+                    if (v != initial[rc] && !tried[cell][c * 9 + v - 1]) { vn_cell[nv] = rc; vn_val[nv] = v; nv++; }
+            }
+            int repaired = 0;
+            for (int k = 0; k < nv && !repaired; k++) {
+                const int value = vn_val[k];
+                int safe = 1;
+                for (int t = 0; t < 9; t++) {
+                    if (temp[i * 9 + t] == value || temp[t * 9 + j] == value) { safe = 0; break; }
+                    if (temp[(3 * (i / 3) + t / 3) * 9 + 3 * (j / 3) + t % 3] == value) { safe = 0; break; }
+                }
+                if (safe) {
+                    const int rc = vn_cell[k];
+                    sudoku[cell] = (uint8_t)value;
+                    partial[cell] = (uint8_t)value;
+                    partial[rc] = 0;
+                    tried[cell][(rc % 9) * 9 + value - 1] = 1;
+                    sudoku[rc] = 0;
+                    queue[--qh] = rc;
+                    repaired = 1;
+                }
+            }
+            if (!repaired) {
+                sudoku[cell] = 0;
+                flag = 0;
+            }
+            if (qh < 1 || qt >= 1024) return -2; /* cannot happen: bounded by the tried sets */
+        }
+        if (!flag) break;                    /* node.py:453-454 */
+        int empty = 0;
+        for (int c = 0; c < 81; c++) empty += sudoku[c] == 0;
+        if (empty < 2) break;                /* node.py:462-464 */
+        *validations = g_val;
+        return -1;                           /* nothing changes any more: the loop spins */
+    }
+    g_val++;                                 /* node.py:466 self.solver.check(self.sudoku) */
+    *validations = g_val;
+    return oracle_check_sums(sudoku) ? 1 : 0;
+}

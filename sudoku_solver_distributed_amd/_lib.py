@@ -17,6 +17,7 @@ SDK_UNSOLVABLE = 0
 SDK_SOLVED = 1
 SDK_INVALID = -1
 SDK_CANCELLED = -2
+SDK_NO_RETURN = -4   # sdk_peer_solve_batch: node.py's /solve loop never returns
 SDK_ORDER_GEN = 0    # gen.py:6-28's walk (last row with an empty cell first)
 SDK_ORDER_NODE = 1   # node.py:62-74's walk (row-major)
 ORDERS = {"gen": SDK_ORDER_GEN, "node": SDK_ORDER_NODE}
@@ -27,6 +28,7 @@ EXPORTS = (
     "sdk_solve_batch",
     "sdk_check_batch",
     "sdk_first_candidate_batch",
+    "sdk_peer_solve_batch",
     "sdk_expand_frontier",
     "sdk_read_stats",
     "sdk_last_error",
@@ -64,6 +66,8 @@ def load() -> ctypes.CDLL:
     L.sdk_check_batch.argtypes = [vp, vp, i64, i32, vp]
     L.sdk_first_candidate_batch.restype = i32
     L.sdk_first_candidate_batch.argtypes = [vp, vp, vp, i64, vp]
+    L.sdk_peer_solve_batch.restype = i32
+    L.sdk_peer_solve_batch.argtypes = [vp, vp, vp, vp, i64, vp]
     L.sdk_expand_frontier.restype = i32
     L.sdk_expand_frontier.argtypes = [vp, i64, vp, vp, vp, i64, i32, vp]
     L.sdk_read_stats.restype = i32

@@ -208,6 +208,38 @@ __global__ __launch_bounds__(256) void first_candidate_kernel(const uint8_t *__r
     num[i] = free_ ? (int32_t)__builtin_ctz(free_) + 1 : 0;
 }
 
+// ------------------------------------------------- reference /solve (greedy)
+// node.py:534-557 P2PNode.peer_sudoku_solve, one thread per board
+// (peer_greedy.h; its ~1.9 KB of state lives in scratch: a cold serving path).
+#include "peer_greedy.h"
+
+__global__ __launch_bounds__(64) void peer_solve_kernel(const uint8_t *__restrict__ boards, uint8_t *__restrict__ out,
+                                                        int32_t *__restrict__ status,
+                                                        int32_t *__restrict__ validations, int64_t n)
+{
+    const int64_t i = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t *src = boards + i * 81;
+    uint8_t *dst = out + i * 81;
+    peer::State s;
+    bool bad = false;
+    for (int k = 0; k < 81; ++k) {
+        s.sudoku[k] = src[k];
+        bad |= s.sudoku[k] > 9;
+    }
+    if (bad) {
+        for (int k = 0; k < 81; ++k) dst[k] = s.sudoku[k];
+        status[i] = SDK_INVALID;
+        validations[i] = 0;
+        return;
+    }
+    int checks = 0;
+    const int r = peer::run(s, checks);
+    for (int k = 0; k < 81; ++k) dst[k] = s.sudoku[k];
+    status[i] = r == peer::PG_CHECKED ? SDK_SOLVED : r == peer::PG_CHECK_FAILED ? SDK_UNSOLVABLE : SDK_NO_RETURN;
+    validations[i] = checks;
+}
+
 // ------------------------------------------------------ frontier expansion
 // pass 1: propagate each node (one wave each), keep the propagated grid and
 // the number of children it will produce.  In node order a node from which
@@ -558,6 +590,20 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
                        d_children, cap, order);
     hipError_t e = hipGetLastError();
     return e == hipSuccess ? 0 : set_err("sdk_expand_frontier: launch", e);
+}
+
+int sdk_peer_solve_batch(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_status, int32_t *d_validations, int64_t n,
+                         void *stream)
+{
+    if (n < 0 || (n > 0 && (!d_boards || !d_out || !d_status || !d_validations))) {
+        snprintf(g_err, sizeof g_err, "sdk_peer_solve_batch: bad arguments");
+        return -2;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(peer_solve_kernel, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, (hipStream_t)stream, d_boards,
+                       d_out, d_status, d_validations, n);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_peer_solve_batch: launch", e);
 }
 
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)

@@ -54,7 +54,7 @@ from typing import List, Optional
 
 import torch
 
-from .solver import SDK_SOLVED, as_boards, get_solver
+from .solver import SDK_NO_RETURN, SDK_SOLVED, as_boards, get_solver
 
 logger = logging.getLogger(__name__)
 
@@ -105,6 +105,12 @@ class GpuSolverBackend:
             return torch.empty((0, 81), dtype=torch.uint8), torch.empty(0, dtype=torch.int32), 0
         return torch.cat(sols), torch.cat(st), sweeps
 
+    def peer_solve(self, boards: torch.Tensor):
+        """The reference's /solve loop per board (sdk_peer_solve_batch):
+        (boards it leaves, status, validations), on the host."""
+        out, st, val = self.solvers[0].peer_solve(as_boards(boards))
+        return out.cpu(), st.cpu(), val.cpu()
+
     def check(self, boards, mode: int):
         return self.solvers[0].check(as_boards(boards, max_value=255), mode).cpu()
 
@@ -115,7 +121,8 @@ class GpuSolverBackend:
 class BoardBatcher:
     """Coalesces concurrent solve requests into one backend call per tick.
 
-    submit() queues (n, 81) boards with a walk order and returns a Future of
+    submit() queues (n, 81) boards with a walk order ("gen", "node", or
+    "peer" for the reference's /solve loop) and returns a Future of
     (solutions, status); one thread drains the queue: it waits for the first
     board, then up to ``max_wait`` seconds (or until ``max_batch`` boards are
     queued) for more, and solves each order's boards in one call."""
@@ -183,7 +190,11 @@ class BoardBatcher:
                 group = [it for it in items if it[1] == order]
                 try:
                     boards = torch.cat([it[0] for it in group])
-                    sols, st, passes = self.backend.solve(boards, order)
+                    if order == "peer":
+                        sols, st, val = self.backend.peer_solve(boards)
+                        passes = int(val.sum())
+                    else:
+                        sols, st, passes = self.backend.solve(boards, order)
                     self.batches += 1
                     self.boards += boards.shape[0]
                     if self.on_batch is not None:
@@ -197,6 +208,10 @@ class BoardBatcher:
                     for _, _, fut in group:
                         if not fut.done():
                             fut.set_exception(e)
+
+
+class ReferenceNoReturn(RuntimeError):
+    """The reference's /solve loop (node.py:427-475) never returns on this board."""
 
 
 def _flat(board):
@@ -314,7 +329,10 @@ class P2PNode:
 
     def __init__(self, host, port, anchor_node=None, handicap=0.001, backend=None,
                  forward_threshold: Optional[int] = None, forward_timeout: float = 10.0,
-                 max_wait: float = 0.0005):
+                 max_wait: float = 0.0005, solve_mode: str = "walk"):
+        if solve_mode not in ("walk", "reference"):
+            raise ValueError("solve_mode must be 'walk' or 'reference'")
+        self.solve_mode = solve_mode
         self.solver = SudokuSolver(handicap, backend=backend, max_wait=max_wait)
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         self.sock.settimeout(0.2)
@@ -483,6 +501,16 @@ class P2PNode:
                 self.served += boards.shape[0]
             reply = {"type": "solution", "sudokus": ["".join(map(str, r.tolist())) for r in sols],
                      "status": st.tolist(), "address": self.id}
+        elif msg.get("mode") == "reference":  # a whole board, the reference's /solve loop
+            board = [row[:] for row in sudoku]
+            try:
+                out = self._reference_solve(board)
+                reply = {"type": "solution", "sudoku": out, "solved": True, "address": self.id}
+            except ReferenceNoReturn:
+                reply = {"type": "solution", "sudoku": board, "solved": False, "no_return": True,
+                         "address": self.id}
+            with self.lock:
+                self.served += 1
         else:  # a whole board handed over by a peer
             board = [row[:] for row in sudoku]
             out = self.solver.solve_sudoku(board)
@@ -494,9 +522,13 @@ class P2PNode:
         self.send(msg["address"], reply)
         self.broadcast_stats_soon()
 
-    def request_solve(self, peer, sudoku, timeout=10.0):
-        """Hand a whole board to `peer` over UDP and wait for its solution."""
-        return self._request(peer, {"type": "solve", "sudoku": sudoku}, timeout)
+    def request_solve(self, peer, sudoku, timeout=10.0, mode=None):
+        """Hand a whole board to `peer` over UDP and wait for its solution
+        (mode "reference": the peer runs the reference's /solve loop)."""
+        msg = {"type": "solve", "sudoku": sudoku}
+        if mode:
+            msg["mode"] = mode
+        return self._request(peer, msg, timeout)
 
     def request_solve_many(self, peer, boards81: List[str], order="node", timeout=10.0):
         """Hand a batch of boards (81-character strings) to `peer`."""
@@ -525,26 +557,50 @@ class P2PNode:
             return None
         return peers[next(self._rr) % len(peers)]
 
+    def _reference_solve(self, board):
+        """node.py:534-557 exactly (solve_mode "reference"): the greedy cell
+        loop on the GPU (sdk_peer_solve_batch).  Returns the board it leaves,
+        valid or not, and counts one solved puzzle either way (node.py:467-
+        474); raises ReferenceNoReturn where node.py never returns."""
+        sols, st = self.solver.batcher.submit(as_boards(_flat(board)), "peer").result()
+        if int(st[0]) == SDK_NO_RETURN:
+            raise ReferenceNoReturn("the reference's /solve loop never returns on this board (node.py:429-464)")
+        with self.solver.lock:
+            self.solver.solved_puzzles += 1
+        _copy_into(board, sols[0].tolist())
+        return board
+
     def peer_sudoku_solve(self, sudoku):
         """node.py:534-557: solve one board for an HTTP client -- on this
-        peer's GPUs, or on a peer's when this one is overloaded."""
+        peer's GPUs, or on a peer's when this one is overloaded.  solve_mode
+        "walk" (default) answers with node.py's recursive walk
+        (SudokuSolver.solve_sudoku) or None; "reference" reproduces the
+        reference's greedy /solve loop."""
         board = [row[:] for row in sudoku]
         peer = self._forward_target()
+        mode = "reference" if self.solve_mode == "reference" else None
         out = None
         if peer is not None:
             try:
-                rep = self.request_solve(peer, board, timeout=self.forward_timeout)
+                rep = self.request_solve(peer, board, timeout=self.forward_timeout, mode=mode)
                 with self.lock:
                     self.forwarded += 1
+                self.broadcast_stats_soon()
+                if rep.get("no_return"):
+                    raise ReferenceNoReturn("the reference's /solve loop never returns on this board")
                 if rep.get("solved"):
                     _copy_into(board, _flat(rep["sudoku"]))
                     out = board
-                self.broadcast_stats_soon()
                 return out
             except TimeoutError:
                 logger.warning("peer %s timed out, solving locally", peer)
-        out = self.solver.solve_sudoku(board)
-        self.broadcast_stats_soon()
+        try:
+            if mode:
+                out = self._reference_solve(board)
+            else:
+                out = self.solver.solve_sudoku(board)
+        finally:
+            self.broadcast_stats_soon()
         return out
 
     def get_stats(self):
@@ -624,7 +680,10 @@ class SudokuHTTPServer(BaseHTTPRequestHandler):
         except Exception as e:
             return self._send_response({"error": f"bad request: {e}"}, 400)
         t0 = time.time()
-        solution = self.p2p_node.peer_sudoku_solve(sudoku)
+        try:
+            solution = self.p2p_node.peer_sudoku_solve(sudoku)
+        except ReferenceNoReturn as e:  # node.py would never answer
+            return self._send_response({"error": str(e), "solution": None}, 500)
         logger.info("Execution time: %s", time.time() - t0)
         if solution:
             self._send_response(solution)
@@ -660,11 +719,15 @@ def main(argv=None):
     ap.add_argument("--gpus", default=None, help="comma list of local GPU indices (default: current)")
     ap.add_argument("--forward-threshold", type=int, default=None,
                     help="hand new boards to peers while this many wait for the local GPUs")
+    ap.add_argument("--solve-mode", choices=("walk", "reference"), default="walk",
+                    help="/solve answer: node.py's recursive walk (default) or the reference's greedy "
+                         "peer_sudoku_solve loop, bit for bit (INTEGRATION.md §3)")
     args = ap.parse_args(argv)
     logging.basicConfig(level=logging.INFO, format="%(asctime)s - %(levelname)s - %(message)s")
     devices = [int(x) for x in args.gpus.split(",")] if args.gpus else None
     node = P2PNode(args.host, args.s, anchor_node=args.a, handicap=args.h / 100,
-                   backend=GpuSolverBackend(devices), forward_threshold=args.forward_threshold)
+                   backend=GpuSolverBackend(devices), forward_threshold=args.forward_threshold,
+                   solve_mode=args.solve_mode)
     node.bind()
     httpd = make_http_server(node, args.host, args.p)
     threading.Thread(target=httpd.serve_forever, daemon=True).start()

@@ -17,11 +17,11 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import SDK_CANCELLED, SDK_INVALID, SDK_SOLVED, SDK_UNSOLVABLE, SudokuHipError
+from ._lib import SDK_CANCELLED, SDK_INVALID, SDK_NO_RETURN, SDK_SOLVED, SDK_UNSOLVABLE, SudokuHipError
 
 __all__ = [
     "BatchSolver", "get_solver", "as_boards", "SDK_SOLVED", "SDK_UNSOLVABLE",
-    "SDK_INVALID", "SDK_CANCELLED", "SudokuHipError",
+    "SDK_INVALID", "SDK_CANCELLED", "SDK_NO_RETURN", "SudokuHipError",
 ]
 
 
@@ -150,6 +150,22 @@ class BatchSolver:
                                                     self._stream(stream))
         _lib.check(rc, "sdk_first_candidate_batch")
         return num
+
+    def peer_solve(self, boards, stream=None):
+        """node.py:534-557 P2PNode.peer_sudoku_solve (the reference's HTTP
+        /solve greedy loop) per board: (boards it leaves (n,81), status (n,),
+        validations (n,)); status SDK_SOLVED / SDK_UNSOLVABLE (check passed /
+        failed) or SDK_NO_RETURN (node.py never returns on that board)."""
+        g = self._dev(as_boards(boards))
+        n = g.shape[0]
+        out = torch.empty_like(g)
+        st = torch.empty(n, dtype=torch.int32, device=self.device)
+        val = torch.empty(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_peer_solve_batch(g.data_ptr(), out.data_ptr(), st.data_ptr(), val.data_ptr(), n,
+                                               self._stream(stream))
+        _lib.check(rc, "sdk_peer_solve_batch")
+        return out, st, val
 
     def expand(self, nodes, order="gen", stream=None) -> torch.Tensor:
         """One frontier level (sdk_expand_frontier); synchronises to size it."""

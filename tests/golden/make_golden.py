@@ -32,7 +32,7 @@ inputs + outputs as JSON data (no reference source is copied):
                          reference's HTTP /solve path, on a fresh single node
                          with handicap 0 (no peers: every cell task runs
                          locally, node.py:443-449): README puzzle + gen boards.
-                         Its answer can be partial or invalid; a 5 s alarm
+                         Its answer can be partial or invalid; a 3 s alarm
                          records the boards on which it never returns.
 """
 from __future__ import annotations
@@ -277,13 +277,17 @@ def main(ref_dir, stages):
     if "peer" in stages:
         boards = [("readme", NAMED["readme"])]
         boards += [(f"gen{c['seed']}", c["puzzle"]) for c in gen_cases
-                   if c["empty_boxes"] in (5, 20, 40) and c["seed"] // 1000 < 6]
+                   if c["empty_boxes"] in (5, 20, 40, 50, 58, 64)]
+        sc_path = os.path.join(HERE, "golden_sc.json")
+        if os.path.exists(sc_path):
+            with open(sc_path) as f:
+                boards += [(f"sc{k}", c["puzzle"]) for k, c in enumerate(json.load(f)[:16])]
         peer_cases = []
         for name, p in boards:
             with contextlib.redirect_stdout(io.StringIO()):
                 n = node.P2PNode("127.0.0.1", 0, handicap=0)
                 try:
-                    out = run_limited(lambda: n.peer_sudoku_solve(b81(p)), 5)
+                    out = run_limited(lambda: n.peer_sudoku_solve(b81(p)), 3)
                     res = s81(out) if out else None
                 except _Timeout:
                     res = "TIMEOUT"
