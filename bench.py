@@ -296,6 +296,14 @@ def main():
                 roof["valu_per_pass"] = vpp
                 roof["useful_lane_frac"] = useful / ops
                 roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
+            # the pass's own ceiling at the kernel's occupancy (microbenchmark)
+            ceil = os.path.join(PMC_DIR, "r02_pass_ceiling.json")
+            if kname == "plane_kernel" and os.path.exists(ceil):
+                with open(ceil) as f:
+                    c = json.load(f)
+                cp = c["by_waves_per_simd"][str(c["plane_kernel_waves_per_simd"])]["passes_per_s"]
+                roof["pass_ceiling_passes_per_s"] = cp
+                roof["pass_ceiling_frac"] = st["sweeps"] / args.steps / kern_s / cp
 
     cpu = None
     if world == 1 and not args.no_cpu:

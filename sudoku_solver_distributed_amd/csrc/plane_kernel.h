@@ -33,12 +33,15 @@
 #include "packed_solver.h"
 
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
-// $SDK_PLANE_TAIL)
+// $SDK_PLANE_TAIL, $SDK_PLANE_DONATE)
 #ifndef SDK_PLANE_REFILL
 #define SDK_PLANE_REFILL 12
 #endif
 #ifndef SDK_PLANE_TAIL
 #define SDK_PLANE_TAIL 2
+#endif
+#ifndef SDK_PLANE_DONATE
+#define SDK_PLANE_DONATE 0
 #endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
@@ -220,6 +223,38 @@ __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__
     return shift;
 }
 
+// ---- drain mailbox (one per workgroup, LDS; SDK_PLANE_DONATE > 0)
+// Once the queue is empty a pass still costs a wave the same whatever its
+// active lanes.  A drained wave down to `donate` boards or fewer offers them
+// to its workgroup's other waves -- only when their published idle lanes can
+// take them at once -- and exits; drained waves take offered boards into
+// idle lanes at every iteration.  A board travels as its 27 plane words,
+// index, depth, guess count and stack SLOT (stacks are addressed by slot, so
+// the stack does not move).  The block's last live wave never offers.
+enum { MB_CAP = 64, MB_WORDS = 32 };  // record: 27 planes, p lo / hi, depth, slot offset, guesses
+struct PlaneMailbox {
+    uint32_t w[MB_WORDS][MB_CAP];  // record r's word k at w[k][r]
+    uint32_t lock, count, live, pad;
+    uint32_t idle[PLANE_THREADS / 64];  // idle lanes each drained wave can take (0 otherwise)
+};
+
+// lane 0 only
+__device__ __forceinline__ void mb_lock(PlaneMailbox &mb)
+{
+    while (atomicCAS(&mb.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+__device__ __forceinline__ void mb_unlock(PlaneMailbox &mb)
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    atomicExch(&mb.lock, 0u);
+}
+// lanes of `mask` below this lane
+__device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
+{
+    return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -242,15 +277,26 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail)
+    int order, int refill, int tail, int donate)
 {
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
+    __shared__ PlaneMailbox mb;
+    const int wid = threadIdx.x >> 6;
+    if (donate > 0) {
+        if (threadIdx.x < PLANE_THREADS / 64) mb.idle[threadIdx.x] = 0;
+        if (threadIdx.x == 0) {
+            mb.lock = 0;
+            mb.count = 0;
+            mb.live = PLANE_THREADS / 64;
+        }
+        __syncthreads();
+    }
     __shared__ uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     const uint8_t *stage_b = (const uint8_t *)stage;
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
-    const PlaneStack stk = {
+    PlaneStack stk = {
         __builtin_amdgcn_make_buffer_rsrc(stack, 0, (int)(nt * PLANE_MAX_DEPTH * 128), 0x00020000),
         (uint32_t)g * (uint32_t)(PLANE_MAX_DEPTH * 128)};
     const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
@@ -316,39 +362,72 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             st_after++;
         }
 #endif
+        if (drained && donate > 0) {
+            // ---- drain mailbox: publish idle lanes, take offered boards
+            const uint64_t idle = __builtin_amdgcn_ballot_w64(state == PL_IDLE);
+            if (lane == 0) mb.idle[wid] = (uint32_t)__builtin_popcountll(idle);
+            if (idle && __hip_atomic_load(&mb.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
+                uint32_t base = 0, take = 0;
+                if (lane == 0) {
+                    mb_lock(mb);
+                    const uint32_t c = mb.count, ni = (uint32_t)__builtin_popcountll(idle);
+                    take = c < ni ? c : ni;
+                    base = c - take;
+                    mb.count = base;
+                }
+                take = rdlane(take, 0);
+                const uint32_t rk = lanes_below(idle);
+                if (state == PL_IDLE && rk < take) {
+                    const uint32_t r = rdlane(base, 0) + rk;
+#pragma unroll
+                    for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = mb.w[w][r];
+                    B.Det[0] = B.Det[1] = B.Det[2] = 0;
+                    p = (int64_t)(((uint64_t)mb.w[28][r] << 32) | mb.w[27][r]);
+                    depth = mb.w[29][r];
+                    stk.lane_off = mb.w[30][r];
+                    bguess = mb.w[31][r];
+                    guesses += bguess;
+                    state = PL_ACTIVE;
+                }
+                if (lane == 0) mb_unlock(mb);
+            }
+        }
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
         if (__builtin_popcountll(~active) >= refill || active == 0) {
             const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
-            // ---- store finished boards, one at a time over the whole wave
+            // ---- store finished boards.  Every solved lane first writes its
+            // board's value bit-slices (digit bit k of every cell, per band:
+            // 12 words) to the LDS staging area, all lanes at once; then the
+            // wave stores one board at a time, each lane reading the slices
+            // of its two cells' bands (same words for every lane: broadcast).
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
             solved += state == PL_SOLVED;
-            while (m) {
-                const int i = __builtin_ctzll(m);
-                m &= m - 1;
-                const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
-                uint8_t *dst = sols + pi * 81;
-                const uint32_t pos = lane & 31;
-                uint32_t v0 = 0, v1 = 0;
+            if (m) {
+                if (state == PL_SOLVED) {
 #pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    // value bit-slices of lane i's (solved) band b, wave-uniform
-                    uint32_t q[9];
-#pragma unroll
-                    for (int d = 0; d < 9; ++d) q[d] = rdlane(B.P[d][b], i);
-                    const uint32_t V[4] = {q[0] | q[2] | q[4] | q[6] | q[8],  // digits 1 3 5 7 9
-                                           q[1] | q[2] | q[5] | q[6],         // 2 3 6 7
-                                           q[3] | q[4] | q[5] | q[6],         // 4 5 6 7
-                                           q[7] | q[8]};                      // 8 9
-                    uint32_t v = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v |= ((V[k] >> pos) & 1u) << k;
-                    if (b == 0) v0 = lane < 32 ? v : v0;
-                    if (b == 1) v0 = lane >= 32 ? v : v0;
-                    if (b == 2) v1 = v;
+                    for (int b = 0; b < 3; ++b) {
+                        stage[(0 * 3 + b) * 64 + lane] = B.P[0][b] | B.P[2][b] | B.P[4][b] | B.P[6][b] | B.P[8][b];
+                        stage[(1 * 3 + b) * 64 + lane] = B.P[1][b] | B.P[2][b] | B.P[5][b] | B.P[6][b];
+                        stage[(2 * 3 + b) * 64 + lane] = B.P[3][b] | B.P[4][b] | B.P[5][b] | B.P[6][b];
+                        stage[(3 * 3 + b) * 64 + lane] = B.P[7][b] | B.P[8][b];
+                    }
                 }
-                if (c0 >= 0) dst[c0] = (uint8_t)v0;
-                if (c1 >= 0) dst[c1] = (uint8_t)v1;
-                if (lane == 0) status[pi] = SDK_SOLVED;
+                const uint32_t pos = lane & 31, b0 = (uint32_t)lane >> 5;  // slot 0: band 0 / 1, slot 1: band 2
+                while (m) {
+                    const int i = __builtin_ctzll(m);
+                    m &= m - 1;
+                    const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                    uint8_t *dst = sols + pi * 81;
+                    uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        v0 |= ((stage[(3 * k + b0) * 64 + i] >> pos) & 1u) << k;
+                        v1 |= ((stage[(3 * k + 2) * 64 + i] >> pos) & 1u) << k;
+                    }
+                    if (c0 >= 0) dst[c0] = (uint8_t)v0;
+                    if (c1 >= 0) dst[c1] = (uint8_t)v1;
+                    if (lane == 0) status[pi] = SDK_SOLVED;
+                }
             }
             // ---- unsolvable / cancelled: the input board back
             m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
@@ -433,7 +512,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // passes; instead it restarts each of them on the wave-per-board
             // solver (packed_solver.h, ~one pass's worth of instructions per
             // board) and exits.
-            if (drained && tail > 0) {
+            if (drained && tail > 0 && (donate <= 0 || mb.live == 1)) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
                 if (act && __builtin_popcountll(act) <= tail) {
                     if (state == PL_ACTIVE) guesses -= bguess;  // those searches start over
@@ -441,7 +520,60 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     break;
                 }
             }
-            if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;
+            if (drained && donate > 0) {
+                // ---- offer this wave's boards if the others can take them now
+                const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
+                const uint32_t na = (uint32_t)__builtin_popcountll(act);
+                if (na > 0 && na <= (uint32_t)donate) {
+                    uint32_t ok = 0, base = 0;
+                    if (lane == 0) {
+                        mb_lock(mb);
+                        uint32_t room = 0;
+#pragma unroll
+                        for (int w = 0; w < PLANE_THREADS / 64; ++w) room += w == wid ? 0u : mb.idle[w];
+                        if (mb.live > 1 && mb.count + na <= room && mb.count + na <= (uint32_t)MB_CAP) {
+                            base = mb.count;
+                            mb.count = base + na;
+                            mb.live -= 1;
+                            mb.idle[wid] = 0;
+                            ok = 1;
+                        } else {
+                            mb_unlock(mb);
+                        }
+                    }
+                    if (rdlane(ok, 0)) {
+                        if (state == PL_ACTIVE) {
+                            const uint32_t r = rdlane(base, 0) + lanes_below(act);
+#pragma unroll
+                            for (int w = 0; w < 27; ++w) mb.w[w][r] = B.P[w / 3][w % 3];
+                            mb.w[27][r] = (uint32_t)p;
+                            mb.w[28][r] = (uint32_t)(p >> 32);
+                            mb.w[29][r] = depth;
+                            mb.w[30][r] = stk.lane_off;
+                            mb.w[31][r] = bguess;
+                            guesses -= bguess;  // counted by the wave that finishes it
+                            state = PL_IDLE;
+                        }
+                        if (lane == 0) mb_unlock(mb);
+                        break;
+                    }
+                }
+            }
+            if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) {
+                // nothing left here: leave, unless boards wait in the mailbox
+                uint32_t leave = 1;
+                if (donate > 0 && lane == 0) {
+                    mb_lock(mb);
+                    if (mb.count == 0) {
+                        mb.live -= 1;
+                        mb.idle[wid] = 0;
+                    } else {
+                        leave = 0;
+                    }
+                    mb_unlock(mb);
+                }
+                if (rdlane(leave, 0)) break;
+            }
         }
         if (state != PL_ACTIVE) continue;
 
