@@ -3,9 +3,11 @@
 mkdir -p gpurun_out
 export TMPDIR=/tmp
 B=${BATCH:-1048576}
-CMD="python -u bench.py --steps 2 --warmup 1 --batch $B --no-cpu --latency-boards 0 --no-extras"
+W=${WORKLOAD:-hard17}
+CMD="python -u bench.py --steps 2 --warmup 1 --batch $B --no-cpu --latency-boards 0 --no-extras --workload $W"
 run() {  # name counters...
   local name=$1; shift
+  rm -rf gpurun_out/pmc_$name
   timeout -s KILL 120 rocprofv3 --pmc "$@" -d gpurun_out/pmc_$name -o run --output-format csv -- $CMD > gpurun_out/pmc_$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"; return $rc
 }
@@ -14,4 +16,6 @@ run wait SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_LDS
 run fetch FETCH_SIZE || exit 1
 run write WRITE_SIZE || exit 1
 K=${PMC_KERNEL:-plane_kernel}
-PMC_KERNEL=$K python scripts/pmc_summarize.py gpurun_out/pmc_$K.json $B 2024 gpurun_out/pmc_valu gpurun_out/pmc_wait gpurun_out/pmc_fetch gpurun_out/pmc_write
+OUT=gpurun_out/pmc_$K.json
+[ "$W" != hard17 ] && OUT=gpurun_out/pmc_${K}_$W.json
+PMC_WORKLOAD=$W PMC_KERNEL=$K python scripts/pmc_summarize.py $OUT $B 2024 gpurun_out/pmc_valu gpurun_out/pmc_wait gpurun_out/pmc_fetch gpurun_out/pmc_write

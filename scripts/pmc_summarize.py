@@ -43,6 +43,7 @@ def main():
             vals[name].append(v)
     summary = {k: sum(v) / len(v) for k, v in vals.items()}
     res = {"kernel": kernel or "plane_kernel", "batch": batch, "seed": seed,
+           "workload": os.environ.get("PMC_WORKLOAD", "hard17"),
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),
            "hbm_bytes_per_launch": None}
