@@ -43,6 +43,12 @@
 #ifndef SDK_PLANE_DONATE
 #define SDK_PLANE_DONATE 0
 #endif
+#ifndef SDK_PLANE_PUSH_PAD
+#define SDK_PLANE_PUSH_PAD 1
+#endif
+#ifndef SDK_PLANE_LDS_STORE
+#define SDK_PLANE_LDS_STORE 1
+#endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
 // plus the loop iterations after the drain, into the second half of the
@@ -75,15 +81,25 @@ struct PlaneStack {
         const int v = (int)voff(level);
 #define PQ(a, b, c, d) (sdk_v4u){opaque(B.P[a / 3][a % 3]), opaque(B.P[b / 3][b % 3]), opaque(B.P[c / 3][c % 3]), \
                                  opaque(B.P[d / 3][d % 3])}
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(0, 1, 2, 3), rsrc, v, 0, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(4, 5, 6, 7), rsrc, v, 16, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(8, 9, 10, 11), rsrc, v, 32, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(12, 13, 14, 15), rsrc, v, 48, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(16, 17, 18, 19), rsrc, v, 64, 0);
-        __builtin_amdgcn_raw_buffer_store_b128(PQ(20, 21, 22, 23), rsrc, v, 80, 0);
+        const sdk_v4u q0 = PQ(0, 1, 2, 3), q1 = PQ(4, 5, 6, 7), q2 = PQ(8, 9, 10, 11), q3 = PQ(12, 13, 14, 15),
+                      q4 = PQ(16, 17, 18, 19), q5 = PQ(20, 21, 22, 23),
+                      q6 = (sdk_v4u){opaque(B.P[8][0]), opaque(B.P[8][1]), opaque(B.P[8][2]), entry};
 #undef PQ
-        __builtin_amdgcn_raw_buffer_store_b128(
-            (sdk_v4u){opaque(B.P[8][0]), opaque(B.P[8][1]), opaque(B.P[8][2]), entry}, rsrc, v, 96, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q0, rsrc, v, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q1, rsrc, v, 16, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q2, rsrc, v, 32, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q3, rsrc, v, 48, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q4, rsrc, v, 64, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q5, rsrc, v, 80, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(q6, rsrc, v, 96, 0);
+#if SDK_PLANE_PUSH_PAD
+        // a dwordx4 store reads its data registers after issue; hipcc pads a
+        // following VALU write of them only when soffset is an inline constant,
+        // and with a register soffset (offsets past 64) it has reused them at
+        // once.  Keeping all seven quads live through a 2-state pad makes
+        // every store read its data before any of them is overwritten.
+        asm volatile("s_nop 1" ::"v"(q0), "v"(q1), "v"(q2), "v"(q3), "v"(q4), "v"(q5), "v"(q6));
+#endif
     }
     // the last quad: planes 24..26 and the branch entry
     __device__ __forceinline__ sdk_v4u top(uint32_t level) const
@@ -209,6 +225,10 @@ __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__
     const __amdgpu_buffer_rsrc_t rsrc =
         __builtin_amdgcn_make_buffer_rsrc((void *)(puzzles + a0), 0, (int)nrec, 0x00020000);
     const uint32_t nd = (shift + 81u * (uint32_t)k + 3u) / 4u;
+    // the DMA writes LDS through the memory path, unordered with this wave's
+    // earlier ds_writes to the same area (the store path's bit-slices):
+    // those must have landed first
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     for (uint32_t i = 0; i < nd; i += 64)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t *)(stage + i), 4, (int)((i + lane) * 4u), 0, 0, 0);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -402,6 +422,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // of its two cells' bands (same words for every lane: broadcast).
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
             solved += state == PL_SOLVED;
+#if SDK_PLANE_LDS_STORE
             if (m) {
                 if (state == PL_SOLVED) {
 #pragma unroll
@@ -429,6 +450,33 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     if (lane == 0) status[pi] = SDK_SOLVED;
                 }
             }
+#else
+            while (m) {
+                const int i = __builtin_ctzll(m);
+                m &= m - 1;
+                const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                uint8_t *dst = sols + pi * 81;
+                const uint32_t pos = lane & 31;
+                uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+                for (int b = 0; b < 3; ++b) {
+                    uint32_t q[9];
+#pragma unroll
+                    for (int d = 0; d < 9; ++d) q[d] = rdlane(B.P[d][b], i);
+                    const uint32_t V[4] = {q[0] | q[2] | q[4] | q[6] | q[8], q[1] | q[2] | q[5] | q[6],
+                                           q[3] | q[4] | q[5] | q[6], q[7] | q[8]};
+                    uint32_t v = 0;
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) v |= ((V[k] >> pos) & 1u) << k;
+                    if (b == 0) v0 = lane < 32 ? v : v0;
+                    if (b == 1) v0 = lane >= 32 ? v : v0;
+                    if (b == 2) v1 = v;
+                }
+                if (c0 >= 0) dst[c0] = (uint8_t)v0;
+                if (c1 >= 0) dst[c1] = (uint8_t)v1;
+                if (lane == 0) status[pi] = SDK_SOLVED;
+            }
+#endif
             // ---- unsolvable / cancelled: the input board back
             m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
             while (m) {
@@ -512,9 +560,21 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // passes; instead it restarts each of them on the wave-per-board
             // solver (packed_solver.h, ~one pass's worth of instructions per
             // board) and exits.
-            if (drained && tail > 0 && (donate <= 0 || mb.live == 1)) {
+            if (drained && tail > 0) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                if (act && __builtin_popcountll(act) <= tail) {
+                uint32_t go = act && __builtin_popcountll(act) <= tail;
+                if (go && donate > 0) {
+                    // with the mailbox on, only the block's last live wave, and only
+                    // with nothing offered (a sibling may have just offered boards)
+                    if (lane == 0) {
+                        mb_lock(mb);
+                        go = mb.live == 1 && mb.count == 0;
+                        if (go) mb.live = 0;
+                        mb_unlock(mb);
+                    }
+                    go = rdlane(go, 0);
+                }
+                if (go) {
                     if (state == PL_ACTIVE) guesses -= bguess;  // those searches start over
                     tail_act = act;
                     break;

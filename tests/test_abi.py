@@ -56,3 +56,18 @@ def test_solver_raises_without_gpu():
     from sudoku_solver_distributed_amd.solver import BatchSolver, SudokuHipError
     with pytest.raises(SudokuHipError):
         BatchSolver()
+
+
+def test_no_wide_store_data_hazard():
+    """Every >64-bit store in the product kernels has a wait state before its
+    data registers are rewritten (scripts/store_hazard_check.py: hipcc does
+    not pad buffer stores with a register soffset; plane_kernel.h
+    PlaneStack::push pads its own)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "scripts"))
+    import store_hazard_check as H
+    assert H.scan(["buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen",
+                   "v_bitop3_b32 v1, v28, 1, v56 bitop3:0x80"])  # the pattern that corrupted the stack
+    assert not H.scan(["buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen", "s_nop 1",
+                       "v_mov_b32 v1, v2"])
+    assert H.main() == 0
