@@ -86,6 +86,50 @@ PS_FN constexpr int cell_pos(int i) { return 10 * ((i / 9) % 3) + i % 9; }
 // cell index of (band, bit position)
 PS_FN int pos_cell(int b, int pos) { return 27 * b + 9 * (pos / 10) + pos % 10; }
 
+// ---- three-input logic at full issue rate
+// gfx950 issues a wave64 VALU instruction every 2 cycles only for some forms
+// (scripts/microbench/exec_rate.hip, profiles/r02_valu_rates.json): VOP2
+// and/or/xor/add/sub/lshrrev with VGPR, inline or literal operands, and
+// v_bitop3_b32 with VGPR or inline operands.  Every form reading an SGPR,
+// v_or3 / v_and_or / v_bfi / v_bfe / v_lshl* and the multiplies take 4.
+// LLVM builds 3-input logic from v_or3 / v_bfi / v_and_or and keeps
+// constants in SGPRs, so the pass spells its 3-input logic as v_bitop3_b32
+// on VGPR operands (truth table f(0xF0, 0xCC, 0xAA) over src0, src1, src2).
+#if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+// a constant as a VGPR value the compiler cannot turn back into an SGPR
+// operand (a VOP3 on gfx9 takes no literal: LLVM would put it in an SGPR)
+template <uint32_t K>
+__device__ __forceinline__ uint32_t vconst()
+{
+    uint32_t r;
+    asm("v_mov_b32 %0, %1" : "=v"(r) : "i"(K));
+    return r;
+}
+template <unsigned TT>
+__device__ __forceinline__ uint32_t bop3(uint32_t a, uint32_t b, uint32_t c)
+{
+    return __builtin_amdgcn_bitop3_b32(a, b, c, TT);
+}
+#define PS_BOP3(TT, a, b, c, host) bop3<TT>(a, b, c)
+#else
+#define PS_BOP3(TT, a, b, c, host) (host)
+#endif
+PS_FN uint32_t or3(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xFE, a, b, c, a | b | c); }
+PS_FN uint32_t maj3(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xE8, a, b, c, (a & b) | (c & (a | b))); }
+PS_FN uint32_t andn(uint32_t a, uint32_t b) { return PS_BOP3(0x30, a, b, b, a & ~b); }
+PS_FN uint32_t andn2(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0x10, a, b, c, a & ~b & ~c); }
+PS_FN uint32_t and_andn(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0x40, a, b, c, a & b & ~c); }
+PS_FN uint32_t or_and(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xF8, a, b, c, a | (b & c)); }
+PS_FN uint32_t or_andn(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xF4, a, b, c, a | (b & ~c)); }
+PS_FN uint32_t and3(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0x80, a, b, c, a & b & c); }
+PS_FN uint32_t andn_and(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0x70, a, b, c, a & ~(b & c)); }
+PS_FN uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return PS_BOP3(0xCA, m, a, b, (m & a) | (~m & b)); }
+// ~a | b | c: a cell of y is a hidden single if its row has one place (not
+// in a), or its box (b) or its column (c) has one
+PS_FN uint32_t bop3_nor(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xEF, a, b, c, ~a | b | c); }
+// 9-bit set (low 24 bits of c may hold no other bit) times k: one v_mul_u32_u24
+PS_FN uint32_t mul24(uint32_t c, uint32_t k) { return (c & 0xFFFFFFu) * k; }
+
 PS_FN uint32_t spread_rows(uint32_t c) { return c | (c << 10) | (c << 20); }  // 9-bit column set -> 3 rows
 PS_FN uint32_t guard_rows(uint32_t g) { return g - (g >> 9); }               // guard flags -> whole rows
 PS_FN uint32_t row_nonzero(uint32_t y) { return (y + ROWS) & GUARDS; }        // guard set iff row != 0
@@ -97,81 +141,94 @@ PS_FN void pin_board(Board &B);
 // One propagation pass (rules A, B, C above).  Returns DEAD, SOLVED, STUCK
 // (a fixpoint: und[] = the undetermined cells, each with >= 2 candidates) or
 // OPEN (something changed: pass again).
+//
+// Written for the full-rate issue forms (see or3() above): two-input ops
+// with literal constants, three-input logic as v_bitop3_b32 on VGPRs, right
+// shifts only, and one v_mul_u32_u24 per spread of a 9-bit set over three
+// rows.  ~1380 issue slots per pass (profiles/isa_plane_pass.json).
 PS_FN int pass(Board &B, uint32_t und[3])
 {
     uint32_t single[3], nd[3];
     uint32_t dead = 0;
-    // ---- A: determined cells
+    // ---- A: determined cells.  o: >= 1 candidate, t: >= 2 candidates
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
-        uint32_t o = 0, t = 0;
-#pragma unroll
-        for (int d = 0; d < 9; ++d) {
-            t |= o & B.P[d][b];
-            o |= B.P[d][b];
-        }
-        dead |= ROWS & ~o;
-        single[b] = o & ~t;
-        nd[b] = single[b] & ~B.Det[b];
+        // (every 3-input OR spelled as one bitop3: LLVM would fuse the
+        // 2-input ones into v_or3 / v_and_or)
+        uint32_t o = B.P[0][b] | B.P[1][b];
+        const uint32_t m23 = maj3(o, B.P[2][b], B.P[3][b]);
+        o = or3(o, B.P[2][b], B.P[3][b]);
+        const uint32_t m45 = maj3(o, B.P[4][b], B.P[5][b]);
+        o = or3(o, B.P[4][b], B.P[5][b]);
+        uint32_t t = or_and(m23, B.P[0][b], B.P[1][b]);
+        t = or3(t, m45, maj3(o, B.P[6][b], B.P[7][b]));
+        o = or3(o, B.P[6][b], B.P[7][b]);
+        t = or_and(t, o, B.P[8][b]);
+        o |= B.P[8][b];
+        dead = or_andn(dead, ROWS, o);
+        single[b] = andn(o, t);
+        nd[b] = andn(single[b], B.Det[b]);
         B.Det[b] = single[b];
-        und[b] = ROWS & ~single[b];
+        und[b] = andn(ROWS, single[b]);
     }
-    const bool all_single = (single[0] & single[1] & single[2]) == ROWS;
-    const bool any_nd = (nd[0] | nd[1] | nd[2]) != 0;
+    const bool all_single = and3(single[0], single[1], single[2]) == ROWS;
+    const bool any_nd = or3(nd[0], nd[1], nd[2]) != 0;
     pin_board(B);
 
     uint32_t hall[3] = {0u, 0u, 0u};
+    // per unit kind, "d has a place": row guard bits, columns, box bits 0/3/6
     uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
         // hidden singles placed for digits < d this pass leave d's plane
         // (Gauss-Seidel: d sees them); digits < d are fixed up after the loop
-        if (d > 0) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b) B.P[d][b] &= ~hall[b];
-        }
         // ---- B: remove d from the peers of the newly determined cells holding d
         uint32_t x[3], f[3];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
+            if (d > 0) B.P[d][b] = andn(B.P[d][b], hall[b]);
             x[b] = nd[b] & B.P[d][b];
-            f[b] = fold_rows(x[b]);
+            f[b] = or3(x[b], x[b] >> 10, x[b] >> 20);  // bits 0-8: columns holding x (above: junk)
         }
-        const uint32_t cpeer = spread_rows(f[0] | f[1] | f[2]);
+        const uint32_t cpeer = mul24(or3(f[0], f[1], f[2]) & 0x1FFu, 0x100401u);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-            const uint32_t g = f[b] | (f[b] >> 1) | (f[b] >> 2);
-            const uint32_t peer = guard_rows(row_nonzero(x[b])) | cpeer | spread_rows((g & BOXC) * 7u);
-            B.P[d][b] = (peer & x[b]) | (~peer & B.P[d][b]);
+            const uint32_t g = or3(f[b], f[b] >> 1, f[b] >> 2);           // box bits 0/3/6
+            const uint32_t rn = (x[b] + ROWS) & GUARDS;                  // rows holding x
+            const uint32_t peer = or3(rn - (rn >> 9), cpeer, mul24(g & BOXC, 0x701C07u));
+            B.P[d][b] = sel(peer, x[b], B.P[d][b]);
         }
         // ---- C: hidden singles of d; units with no place left for d
-        uint32_t o[3], t[3], hb[3];
+        uint32_t o[3], t[3], gr[3], hb[3];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
             const uint32_t y = B.P[d][b];
-            const uint32_t nzy = row_nonzero(y);
-            const uint32_t nzm = row_nonzero(y & (y + KDEC));  // rows with >= 2 places
-            rowall &= nzy;
-            const uint32_t hr = y & guard_rows(nzy & ~nzm);
+            const uint32_t y1 = y + ROWS;     // row guard set iff the row has a place; = y + KDEC
+            rowall &= y1;
+            const uint32_t z = y & y1;        // y without its lowest place per row
+            const uint32_t nz = (z + ROWS) & GUARDS;
+            gr[b] = nz - (nz >> 9);           // rows with >= 2 places
             const uint32_t s1 = y >> 10, s2 = y >> 20;
-            o[b] = (y | s1 | s2) & 0x1FFu;                        // per column: >= 1 place in the band
-            t[b] = ((y & s1) | (s2 & (y | s1))) & 0x1FFu;        // per column: >= 2 places in the band
+            o[b] = or3(y, s1, s2);            // bits 0-8: columns with >= 1 place in the band
+            t[b] = maj3(y, s1, s2);           //           columns with >= 2
             const uint32_t o1 = o[b] >> 1, o2 = o[b] >> 2;
-            const uint32_t ob = o[b] | o1 | o2;                   // per box (bits 0, 3, 6)
-            const uint32_t tb = t[b] | (t[b] >> 1) | (t[b] >> 2) | (o[b] & o1) | (o2 & (o[b] | o1));
+            const uint32_t ob = or3(o[b], o1, o2);     // box bits 0/3/6: >= 1 place
             boxall &= ob;
-            hb[b] = hr | (y & spread_rows((ob & ~tb & BOXC) * 7u));
+            const uint32_t tb = or3(t[b], t[b] >> 1, t[b] >> 2);
+            const uint32_t q = andn2(ob, tb, maj3(o[b], o1, o2)) & BOXC;  // boxes with exactly one
+            hb[b] = mul24(q, 0x701C07u);
         }
-        const uint32_t O = o[0] | o[1] | o[2];
-        const uint32_t T = t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
+        const uint32_t O = or3(o[0], o[1], o[2]);
         colall &= O;
-        const uint32_t hcol = spread_rows(O & ~T);
-        // d's hidden singles: later digits drop these cells at their turn
-        // (above), earlier ones after the loop.  A cell forced for two
-        // digits loses the later one, whose unit then has no place for it:
-        // dead, as it must be.
+        const uint32_t hc = andn2(O, or3(t[0], t[1], t[2]), maj3(o[0], o[1], o[2])) & 0x1FFu;
+        const uint32_t hcol = mul24(hc, 0x100401u);
+        // d's hidden singles: the cells of y alone in their row, column or
+        // box.  Later digits drop these cells at their turn (above), earlier
+        // ones after the loop.  A cell forced for two digits loses the later
+        // one, whose unit then has no place for it: dead, as it must be.
 #pragma unroll
-        for (int b = 0; b < 3; ++b) hall[b] |= hb[b] | (B.P[d][b] & hcol);
+        for (int b = 0; b < 3; ++b)
+            hall[b] = or_and(hall[b], B.P[d][b], bop3_nor(gr[b], hb[b], hcol));
         pin_board(B);
         // the unit accumulators too: unpinned, the AND / OR chains over the
         // nine digits are re-associated into trees at the end of the pass,
@@ -193,14 +250,14 @@ PS_FN int pass(Board &B, uint32_t und[3])
         uint32_t later = B.P[8][b];
 #pragma unroll
         for (int e = 7; e >= 0; --e) {
-            B.P[e][b] &= ~(hall[b] & later);
+            B.P[e][b] = andn_and(B.P[e][b], hall[b], later);
             if (e) later |= B.P[e][b];
         }
     }
-    dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
+    dead |= or3(rowall ^ GUARDS, colall ^ 0x1FFu, (boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;
     if (all_single) return SOLVED;
-    const bool newh = ((hall[0] & und[0]) | (hall[1] & und[1]) | (hall[2] & und[2])) != 0;
+    const bool newh = or3(hall[0] & und[0], hall[1] & und[1], hall[2] & und[2]) != 0;
     return (any_nd || newh) ? OPEN : STUCK;
 }
 

@@ -116,3 +116,142 @@ extern "C" void plane_solve_stats(const uint8_t *in, int64_t n, int node_order, 
         depth[i] = (int32_t)stk.max_depth;
     }
 }
+
+// ---- the round-2 (pre-bitop3) formulation of plane::pass, restated as the
+// checker of the full-rate rewrite: both must leave the same board state and
+// return the same verdict after every pass (test-only).
+namespace v1 {
+using namespace plane;
+static uint32_t spread(uint32_t c) { return c | (c << 10) | (c << 20); }
+static uint32_t grows(uint32_t g) { return g - (g >> 9); }
+static uint32_t rnz(uint32_t y) { return (y + ROWS) & GUARDS; }
+static uint32_t fold(uint32_t y) { return (y | (y >> 10) | (y >> 20)) & 0x1FFu; }
+static int pass(Board &B, uint32_t und[3])
+{
+    uint32_t single[3], nd[3], dead = 0;
+    for (int b = 0; b < 3; ++b) {
+        uint32_t o = 0, t = 0;
+        for (int d = 0; d < 9; ++d) {
+            t |= o & B.P[d][b];
+            o |= B.P[d][b];
+        }
+        dead |= ROWS & ~o;
+        single[b] = o & ~t;
+        nd[b] = single[b] & ~B.Det[b];
+        B.Det[b] = single[b];
+        und[b] = ROWS & ~single[b];
+    }
+    const bool all_single = (single[0] & single[1] & single[2]) == ROWS;
+    const bool any_nd = (nd[0] | nd[1] | nd[2]) != 0;
+    uint32_t hall[3] = {0u, 0u, 0u};
+    uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
+    for (int d = 0; d < 9; ++d) {
+        if (d > 0)
+            for (int b = 0; b < 3; ++b) B.P[d][b] &= ~hall[b];
+        uint32_t x[3], f[3];
+        for (int b = 0; b < 3; ++b) {
+            x[b] = nd[b] & B.P[d][b];
+            f[b] = fold(x[b]);
+        }
+        const uint32_t cpeer = spread(f[0] | f[1] | f[2]);
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t g = f[b] | (f[b] >> 1) | (f[b] >> 2);
+            const uint32_t peer = grows(rnz(x[b])) | cpeer | spread((g & BOXC) * 7u);
+            B.P[d][b] = (peer & x[b]) | (~peer & B.P[d][b]);
+        }
+        uint32_t o[3], t[3], hb[3];
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t y = B.P[d][b];
+            const uint32_t nzy = rnz(y), nzm = rnz(y & (y + KDEC));
+            rowall &= nzy;
+            const uint32_t hr = y & grows(nzy & ~nzm);
+            const uint32_t s1 = y >> 10, s2 = y >> 20;
+            o[b] = (y | s1 | s2) & 0x1FFu;
+            t[b] = ((y & s1) | (s2 & (y | s1))) & 0x1FFu;
+            const uint32_t o1 = o[b] >> 1, o2 = o[b] >> 2;
+            const uint32_t ob = o[b] | o1 | o2;
+            const uint32_t tb = t[b] | (t[b] >> 1) | (t[b] >> 2) | (o[b] & o1) | (o2 & (o[b] | o1));
+            boxall &= ob;
+            hb[b] = hr | (y & spread((ob & ~tb & BOXC) * 7u));
+        }
+        const uint32_t O = o[0] | o[1] | o[2];
+        const uint32_t T = t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
+        colall &= O;
+        const uint32_t hcol = spread(O & ~T);
+        for (int b = 0; b < 3; ++b) hall[b] |= hb[b] | (B.P[d][b] & hcol);
+    }
+    for (int b = 0; b < 3; ++b) {
+        uint32_t later = B.P[8][b];
+        for (int e = 7; e >= 0; --e) {
+            B.P[e][b] &= ~(hall[b] & later);
+            if (e) later |= B.P[e][b];
+        }
+    }
+    dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
+    if (dead) return DEAD;
+    if (all_single) return SOLVED;
+    const bool newh = ((hall[0] & und[0]) | (hall[1] & und[1]) | (hall[2] & und[2])) != 0;
+    return (any_nd || newh) ? OPEN : STUCK;
+}
+}  // namespace v1
+
+static bool same_state(const plane::Board &a, const plane::Board &b, const uint32_t (&ua)[3], const uint32_t (&ub)[3])
+{
+    for (int d = 0; d < 9; ++d)
+        for (int k = 0; k < 3; ++k)
+            if (a.P[d][k] != b.P[d][k]) return false;
+    for (int k = 0; k < 3; ++k)
+        if (a.Det[k] != b.Det[k] || ua[k] != ub[k]) return false;
+    return true;
+}
+
+// Step plane::pass and v1::pass side by side from (a) each board's loaded
+// planes, branching on the first undetermined cell at a fixpoint, and (b)
+// `nrand` random plane states (any bits in the cell positions, random Det):
+// returns the number of passes whose state or verdict differ.
+extern "C" int64_t plane_check_pass(const uint8_t *in, int64_t n, int64_t nrand, uint64_t seed)
+{
+    int64_t bad = 0;
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t x[21];
+        words_of(in + i * 81, x);
+        plane::Board A, B;
+        bool clash = false;
+        if (!plane::load_words(A, x, clash)) continue;
+        B = A;
+        for (int step = 0; step < 400; ++step) {
+            uint32_t ua[3], ub[3];
+            const int ra = plane::pass(A, ua), rb = v1::pass(B, ub);
+            if (ra != rb || !same_state(A, B, ua, ub)) { bad++; break; }
+            if (ra == plane::DEAD || ra == plane::SOLVED) break;
+            if (ra == plane::STUCK) {
+                int band, pos;
+                plane::pick_cell(ua, 0, band, pos);
+                const uint32_t cand = plane::cell_cand(A, band, pos);
+                const uint32_t d = cand & (0u - cand);
+                plane::set_cell(A, band, pos, d);
+                plane::set_cell(B, band, pos, d);
+            }
+        }
+    }
+    uint64_t s = seed * 0x9E3779B97F4A7C15ull + 1;
+    auto rnd = [&]() { s ^= s << 13; s ^= s >> 7; s ^= s << 17; return (uint32_t)(s >> 11); };
+    for (int64_t i = 0; i < nrand; ++i) {
+        plane::Board A;
+        const int density = (int)(rnd() % 4);  // sparse to dense planes
+        for (int d = 0; d < 9; ++d)
+            for (int k = 0; k < 3; ++k) {
+                uint32_t w = rnd();
+                for (int j = 0; j < density; ++j) w |= rnd();
+                A.P[d][k] = w & plane::ROWS;
+            }
+        for (int k = 0; k < 3; ++k) A.Det[k] = (rnd() & rnd()) & plane::ROWS;
+        plane::Board B = A;
+        for (int step = 0; step < 8; ++step) {
+            uint32_t ua[3], ub[3];
+            const int ra = plane::pass(A, ua), rb = v1::pass(B, ub);
+            if (ra != rb || !same_state(A, B, ua, ub)) { bad++; break; }
+        }
+    }
+    return bad;
+}

@@ -119,3 +119,21 @@ def test_plane_loader_matches_byte_loader(host):
     boards[2] = 9
     boards[3, 80] = 10
     assert host.plane_check_load(boards.ctypes.data, n) == 0
+
+
+def test_pass_matches_previous_formulation(host):
+    """The full-rate pass (v_bitop3 forms, plane_solver.h) leaves the same
+    state and verdict as the previous formulation after every pass: along
+    the search of hard 17-clue and generated boards, and from random plane
+    states (tests/native/plane_host.cpp plane_check_pass)."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    grids, _ = O.solve_unique_batch(hard17_batch(200, seed=13).numpy())
+    rng = np.random.default_rng(13)
+    for g in grids:  # gen.py-style: complete grids with 50 cells erased
+        g[rng.choice(81, 50, replace=False)] = 0
+    host.plane_check_pass.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64]
+    host.plane_check_pass.restype = ctypes.c_int64
+    boards = np.ascontiguousarray(np.concatenate([hard17_batch(300, seed=11).numpy(),
+                                                  hard_search_batch(300, seed=12).numpy(),
+                                                  grids]))
+    assert host.plane_check_pass(boards.ctypes.data, len(boards), 200_000, 99) == 0
