@@ -28,7 +28,7 @@ cap = 1 << 20
 total = int(lib.sdk_workspace_bytes())
 list_off = total - cap * 8
 waves = (min(n, 256 * 4 * 256)) // 64
-st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 32].view(torch.int64).cpu().numpy().reshape(-1, 4)
+st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 128].view(torch.int64).cpu().numpy().reshape(-1, 16)
 t0 = st[:, 0].min()
 us = lambda x: (x - t0) / 100.0  # 100 MHz
 q = [0, 10, 50, 90, 99, 100]
@@ -40,3 +40,10 @@ print("iters after drain pct", q, np.percentile(st[:, 3], q).round(0).tolist())
 ex = np.sort(us(st[:, 2]))
 for frac in (0.25, 0.5, 0.75, 0.9, 0.99):
     print(f"  {frac:.0%} of waves exited by {ex[int(frac * (len(ex) - 1))]:.1f} us")
+life = (st[:, 2] - st[:, 0]) / 100.0
+cyc = st[:, 4] + st[:, 5] + st[:, 6]
+print(f"wave lifetime us: mean {life.mean():.1f}; loop iterations: mean {st[:, 7].mean():.1f}")
+for k, name in ((4, "pass"), (5, "store+refill+control"), (8, "  of which queue atomic"), (9, "  of which span DMA"),
+                (10, "  of which deposit"), (6, "tail restarts")):
+    print(f"  {name:22s} {st[:, k].sum() / cyc.sum():.3f} of stamped cycles, {st[:, k].mean() / 1e3:.1f} kcycles per wave")
+print(f"  stamped kcycles per wave {cyc.mean() / 1e3:.1f} (shader clock; lifetime {life.mean():.1f} us)")

@@ -43,11 +43,11 @@
 #ifndef SDK_PLANE_DONATE
 #define SDK_PLANE_DONATE 0
 #endif
+#ifndef SDK_PLANE_CHUNK
+#define SDK_PLANE_CHUNK 64
+#endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
-#endif
-#ifndef SDK_PLANE_LDS_STORE
-#define SDK_PLANE_LDS_STORE 1
 #endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
@@ -58,6 +58,9 @@
 #endif
 static_assert(plane::STACK_ENTRY == 27, "stack layout");
 typedef uint32_t sdk_v4u __attribute__((ext_vector_type(4)));
+// v_writelane_b32 (this clang has no builtin for it): the LLVM intrinsic,
+// so the compiler places the lane select in m0 and handles the hazards
+__device__ int llvm_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // Per-lane DFS stack in the workspace: level L of lane g is one 128-byte
 // line at byte (g * PLANE_MAX_DEPTH + L) * 128, words 0..26 = the 27 planes
@@ -211,7 +214,10 @@ __device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, u
 // dwords, all in flight together, no VGPRs), so a refill costs one HBM round
 // trip instead of one per board; the per-board ballots then read bytes from
 // LDS.  Bytes past the batch read as 0 (buffer range check).
-enum { PLANE_STAGE_DWORDS = 1344 };  // >= (3 + 64*81 + 3) / 4, rounded up to 64
+// >= (3 + 64*81 + 3) / 4 rounded up to 64 (the span DMA writes whole 64-dword
+// rows), plus one dword the DMA never writes: a zero byte for the refill's
+// cell-less slots (byte offset PLANE_STAGE_ZERO, zeroed at kernel start)
+enum { PLANE_STAGE_DWORDS = 1348, PLANE_STAGE_ZERO = 4 * (PLANE_STAGE_DWORDS - 1) };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
@@ -297,7 +303,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int donate)
+    int order, int refill, int tail, int donate, int chunk)
 {
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     __shared__ PlaneMailbox mb;
@@ -311,9 +317,11 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         }
         __syncthreads();
     }
-    __shared__ uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     const uint8_t *stage_b = (const uint8_t *)stage;
+    sdk_v4u *stage4 = (sdk_v4u *)stage;  // the store path's slice records
+    if ((threadIdx.x & 63) == 0) stage[PLANE_STAGE_DWORDS - 1] = 0u;  // the zero byte
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
     PlaneStack stk = {
@@ -331,21 +339,33 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // over the wave at exit)
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     uint32_t bguess = 0;  // guesses on the current board (dropped if it is handed off)
-    bool drained = false;  // the queue is empty
+    bool drained = false;  // the queue is empty and this wave's reservoir too
+    // Board hand-out.  The first nt boards go out statically, 64 consecutive
+    // ones per wave; the rest through the queue head (board nt + head).  A
+    // wave claims a CHUNK of boards at a time into its reservoir [res_lo,
+    // res_hi) and refills from it: one queue atomic per chunk instead of per
+    // refill (the head is one device-scope atomic for 4096 waves).  Chunks
+    // shrink towards the end of the batch (guided: remaining / (2 waves)).
+    int64_t res_lo = 0, res_hi = 0;
+    bool queue_out = false;
+    const int64_t nwaves = (int64_t)gridDim.x * (PLANE_THREADS / 64);
     uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
 #if SDK_PLANE_STAMPS
     const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t st_t1 = 0;
-    uint32_t st_after = 0;
+    uint32_t st_after = 0, st_iters = 0;
+    // shader-clock cycles spent in the pass step / the store + refill block /
+    // the tail restarts (s_memtime at wave-uniform points)
+    uint64_t st_pass = 0, st_io = 0, st_tail = 0, st_tb = 0;
+    uint64_t st_atom = 0, st_dma = 0, st_dep = 0;  // parts of st_io: queue atomic, span DMA, per-board deposit
 #endif
 
     // Start-up: the wave's first 64 boards arrive as one staged span; each
     // lane then converts its own board (plane::load_words), all lanes at once.
     {
-        unsigned long long base = 0;
-        if (lane == 0) base = atomicAdd(&ws[WS_QUEUE], 64ull);
-        base = rdlane64(base, 0);
-        drained = (int64_t)base + 64 >= n;
+        const unsigned long long base = (unsigned long long)(g - lane);
+        queue_out = nt >= n;
+        drained = queue_out;
         const int64_t q = (int64_t)base + lane;
         const int64_t kk = (int64_t)base < n ? (n - (int64_t)base < 64 ? n - (int64_t)base : 64) : 0;
         const uint32_t sh = kk ? plane_stage_span(puzzles, n, (int64_t)base, (int)kk, stage, lane) : 0u;
@@ -377,6 +397,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
 
     for (;;) {
 #if SDK_PLANE_STAMPS
+        const uint64_t st_ta = __builtin_amdgcn_s_memtime();
+        if (st_tb) st_pass += st_ta - st_tb;
+        st_iters++;
         if (drained) {
             if (!st_t1) st_t1 = __builtin_amdgcn_s_memrealtime();
             st_after++;
@@ -422,15 +445,19 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // of its two cells' bands (same words for every lane: broadcast).
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
             solved += state == PL_SOLVED;
-#if SDK_PLANE_LDS_STORE
             if (m) {
                 if (state == PL_SOLVED) {
+                    // value bit-slice k of band b, shifted left by k (bit pos + k
+                    // = bit k of the value at pos; bit 29 is a guard, so
+                    // nothing is lost), as one 16-byte record per (band, lane)
 #pragma unroll
                     for (int b = 0; b < 3; ++b) {
-                        stage[(0 * 3 + b) * 64 + lane] = B.P[0][b] | B.P[2][b] | B.P[4][b] | B.P[6][b] | B.P[8][b];
-                        stage[(1 * 3 + b) * 64 + lane] = B.P[1][b] | B.P[2][b] | B.P[5][b] | B.P[6][b];
-                        stage[(2 * 3 + b) * 64 + lane] = B.P[3][b] | B.P[4][b] | B.P[5][b] | B.P[6][b];
-                        stage[(3 * 3 + b) * 64 + lane] = B.P[7][b] | B.P[8][b];
+                        const uint32_t v0 = plane::or3(plane::or3(B.P[0][b], B.P[2][b], B.P[4][b]), B.P[6][b], B.P[8][b]);
+                        const uint32_t v1 = plane::or3(B.P[1][b], B.P[2][b], B.P[5][b] | B.P[6][b]);
+                        const uint32_t v2 = plane::or3(B.P[3][b], B.P[4][b], B.P[5][b] | B.P[6][b]);
+                        const uint32_t v3 = B.P[7][b] | B.P[8][b];
+                        const uint32_t v22 = v2 + v2, v33 = v3 + v3 + v3 + v3;
+                        stage4[b * 64 + lane] = (sdk_v4u){v0, v1 + v1, v22 + v22, v33 + v33};
                     }
                 }
                 const uint32_t pos = lane & 31, b0 = (uint32_t)lane >> 5;  // slot 0: band 0 / 1, slot 1: band 2
@@ -439,44 +466,17 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     m &= m - 1;
                     const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
                     uint8_t *dst = sols + pi * 81;
-                    uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        v0 |= ((stage[(3 * k + b0) * 64 + i] >> pos) & 1u) << k;
-                        v1 |= ((stage[(3 * k + 2) * 64 + i] >> pos) & 1u) << k;
-                    }
+                    const sdk_v4u t0 = stage4[b0 * 64 + i], t1 = stage4[2 * 64 + i];
+                    // value = bit k of (slice k << k) >> pos, k = 0..3
+                    const uint32_t v0 = plane::sel(7u, plane::sel(3u, plane::sel(1u, t0.x >> pos, t0.y >> pos), t0.z >> pos),
+                                                   t0.w >> pos) & 15u;
+                    const uint32_t v1 = plane::sel(7u, plane::sel(3u, plane::sel(1u, t1.x >> pos, t1.y >> pos), t1.z >> pos),
+                                                   t1.w >> pos) & 15u;
                     if (c0 >= 0) dst[c0] = (uint8_t)v0;
                     if (c1 >= 0) dst[c1] = (uint8_t)v1;
                     if (lane == 0) status[pi] = SDK_SOLVED;
                 }
             }
-#else
-            while (m) {
-                const int i = __builtin_ctzll(m);
-                m &= m - 1;
-                const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
-                uint8_t *dst = sols + pi * 81;
-                const uint32_t pos = lane & 31;
-                uint32_t v0 = 0, v1 = 0;
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    uint32_t q[9];
-#pragma unroll
-                    for (int d = 0; d < 9; ++d) q[d] = rdlane(B.P[d][b], i);
-                    const uint32_t V[4] = {q[0] | q[2] | q[4] | q[6] | q[8], q[1] | q[2] | q[5] | q[6],
-                                           q[3] | q[4] | q[5] | q[6], q[7] | q[8]};
-                    uint32_t v = 0;
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) v |= ((V[k] >> pos) & 1u) << k;
-                    if (b == 0) v0 = lane < 32 ? v : v0;
-                    if (b == 1) v0 = lane >= 32 ? v : v0;
-                    if (b == 2) v1 = v;
-                }
-                if (c0 >= 0) dst[c0] = (uint8_t)v0;
-                if (c1 >= 0) dst[c1] = (uint8_t)v1;
-                if (lane == 0) status[pi] = SDK_SOLVED;
-            }
-#endif
             // ---- unsolvable / cancelled: the input board back
             m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
             while (m) {
@@ -501,58 +501,107 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 if (lane == 0) status[pi] = cancelled ? SDK_CANCELLED : SDK_UNSOLVABLE;
             }
             if (state != PL_ACTIVE) state = PL_IDLE;
-            // ---- refill the free lanes: one queue add per wave, then one
-            // board at a time over the whole wave
+            // ---- refill the free lanes: one queue add per wave; the boards'
+            // bytes come into LDS as one span (plane_stage_span); then, one
+            // board at a time, six ballots over the wave give its value
+            // bit-slices (slot 0: four, one per value bit; slot 1: two, lanes
+            // 0-31 and 32-63 testing different bits of the same band-2
+            // cell) and v_writelane drops the 12 slice words into the
+            // board's lane, into plane words the idle lane does not use;
+            // finally every loaded lane turns its slices into planes at once
             if (!drained) {
                 const uint64_t idle = ~active;
                 const int k = __builtin_popcountll(idle);
                 unsigned long long base = 0;
                 const int leader = __builtin_ctzll(idle);
-                if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)k);
-                base = __shfl(base, leader);
-                drained = (int64_t)base + k >= n;
-                bool loaded = false;
-                const int kk = (int64_t)base < n ? (int)(n - (int64_t)base < k ? n - (int64_t)base : k) : 0;
-                const uint32_t sh = kk ? plane_stage_span(puzzles, n, (int64_t)base, kk, stage, lane) : 0u;
-                m = idle;
-                for (int64_t q = (int64_t)base; m && q < n; ++q) {
-                    const int i = __builtin_ctzll(m);
-                    m &= m - 1;
-                    if (lane == i) fin++;
-                    const uint8_t *src = puzzles + q * 81;
-                    const uint8_t *sb = stage_b + sh + 81u * (uint32_t)(q - (int64_t)base);
-                    // slots holding no cell read the sentinel 0x100 (no byte value)
-                    const uint32_t a0 = c0 >= 0 ? sb[c0] : 0x100u, a1 = c1 >= 0 ? sb[c1] : 0x100u;
-                    if (__builtin_amdgcn_ballot_w64((a0 > 9 && a0 != 0x100u) || (a1 > 9 && a1 != 0x100u))) {
-                        plane_copy_board(src, sols + q * 81, lane);  // raw input back
-                        if (lane == 0) status[q] = SDK_INVALID;
-                        continue;
+#if SDK_PLANE_STAMPS
+                const uint64_t st_r0 = __builtin_amdgcn_s_memtime();
+#endif
+                if (res_lo == res_hi && !queue_out) {
+                    // guided chunk: this wave's share of what is left, at least k
+                    int64_t c = chunk > 0 ? (n - (res_hi > nt ? res_hi : nt)) / (2 * nwaves) : 0;
+                    c = c > chunk ? chunk : c;
+                    c = c < k ? k : c;
+                    if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)c);
+                    base = __shfl(base, leader);
+                    res_lo = nt + (int64_t)base;
+                    res_hi = res_lo + c < n ? res_lo + c : n;
+                    if (res_lo > n) res_lo = n;
+                    queue_out = res_lo + c >= n;
+                }
+                base = (unsigned long long)res_lo;
+                const int kk = (int)(res_hi - res_lo < k ? res_hi - res_lo : k);
+                res_lo += kk;
+                drained = queue_out && res_lo == res_hi;
+#if SDK_PLANE_STAMPS
+                const uint64_t st_r1 = __builtin_amdgcn_s_memtime();
+                st_atom += st_r1 - st_r0;
+#endif
+                if (kk) {
+                    const uint32_t sh = plane_stage_span(puzzles, n, (int64_t)base, kk, stage, lane);
+#if SDK_PLANE_STAMPS
+                    const uint64_t st_r2 = __builtin_amdgcn_s_memtime();
+                    st_dma += st_r2 - st_r1;
+#endif
+                    const int c1x = plane_slot_cell(lane & 31, 1);  // band 2, both halves
+                    uint32_t ad0 = c0 >= 0 ? sh + (uint32_t)c0 : (uint32_t)PLANE_STAGE_ZERO;
+                    uint32_t ad1 = c1x >= 0 ? sh + (uint32_t)c1x : (uint32_t)PLANE_STAGE_ZERO;
+                    const uint32_t st0 = c0 >= 0 ? 81u : 0u, st1 = c1x >= 0 ? 81u : 0u;
+                    const uint32_t mlo = lane < 32 ? 1u : 2u, mhi = lane < 32 ? 4u : 8u;
+                    uint64_t mm = idle, loaded = 0, bad = 0;
+                    for (int j = 0; j < kk; ++j) {
+                        const int i = __builtin_ctzll(mm);
+                        mm &= mm - 1;
+                        const uint32_t a0 = stage_b[ad0], a1 = stage_b[ad1];
+                        ad0 += st0;
+                        ad1 += st1;
+                        const uint64_t s0 = __builtin_amdgcn_ballot_w64((a0 & 1u) != 0u);
+                        const uint64_t s1 = __builtin_amdgcn_ballot_w64((a0 & 2u) != 0u);
+                        const uint64_t s2 = __builtin_amdgcn_ballot_w64((a0 & 4u) != 0u);
+                        const uint64_t s3 = __builtin_amdgcn_ballot_w64((a0 & 8u) != 0u);
+                        const uint64_t u01 = __builtin_amdgcn_ballot_w64((a1 & mlo) != 0u);
+                        const uint64_t u23 = __builtin_amdgcn_ballot_w64((a1 & mhi) != 0u);
+                        if (__builtin_amdgcn_ballot_w64(a0 > 9u || a1 > 9u)) bad |= 1ull << i;
+                        loaded |= 1ull << i;
+#define PLANE_DROP(d, b, w) B.P[d][b] = (uint32_t)llvm_writelane((int)(uint32_t)(w), i, (int)B.P[d][b])
+                        PLANE_DROP(0, 0, s0); PLANE_DROP(0, 1, s0 >> 32); PLANE_DROP(0, 2, u01);
+                        PLANE_DROP(1, 0, s1); PLANE_DROP(1, 1, s1 >> 32); PLANE_DROP(1, 2, u01 >> 32);
+                        PLANE_DROP(2, 0, s2); PLANE_DROP(2, 1, s2 >> 32); PLANE_DROP(2, 2, u23);
+                        PLANE_DROP(3, 0, s3); PLANE_DROP(3, 1, s3 >> 32); PLANE_DROP(3, 2, u23 >> 32);
+#undef PLANE_DROP
                     }
-                    if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q) {
-                        plane_copy_board(src, sols + q * 81, lane);
-                        if (lane == 0) status[q] = SDK_CANCELLED;
-                        continue;
-                    }
-                    const uint64_t e0 = __builtin_amdgcn_ballot_w64(a0 == 0u);
-                    const uint32_t E[3] = {(uint32_t)e0, (uint32_t)(e0 >> 32),
-                                           (uint32_t)__builtin_amdgcn_ballot_w64(a1 == 0u)};
-#pragma unroll
-                    for (int d = 0; d < 9; ++d) {
-                        const uint64_t m0 = __builtin_amdgcn_ballot_w64(a0 == (uint32_t)(d + 1));
-                        const uint32_t m1 = (uint32_t)__builtin_amdgcn_ballot_w64(a1 == (uint32_t)(d + 1));
-                        B.P[d][0] = lane == i ? ((uint32_t)m0 | E[0]) : B.P[d][0];
-                        B.P[d][1] = lane == i ? ((uint32_t)(m0 >> 32) | E[1]) : B.P[d][1];
-                        B.P[d][2] = lane == i ? (m1 | E[2]) : B.P[d][2];
-                    }
-                    if (lane == i) {
-                        B.Det[0] = B.Det[1] = B.Det[2] = 0;
-                        p = q;
+                    if ((loaded >> lane) & 1u) {
+                        fin++;
+                        p = (int64_t)base + (int64_t)lanes_below(loaded);
                         depth = 0;
                         bguess = 0;
-                        loaded = true;
+                        if (!((bad >> lane) & 1u) &&
+                            !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
+                            uint32_t V[4][3], given[3];
+#pragma unroll
+                            for (int v = 0; v < 4; ++v)
+#pragma unroll
+                                for (int b = 0; b < 3; ++b) V[v][b] = B.P[v][b];
+                            plane::planes_from_slices(B, V, given);
+                            state = PL_ACTIVE;
+                        } else if (!((bad >> lane) & 1u)) {
+                            state = PL_CANCELLED;  // ordered mode: a lower board is solved
+                        }
                     }
+                    // boards with a byte > 9 (or cancelled): the raw input back
+                    uint64_t r = loaded & __builtin_amdgcn_ballot_w64(state != PL_ACTIVE);
+                    while (r) {
+                        const int i = __builtin_ctzll(r);
+                        r &= r - 1;
+                        const int64_t q = (int64_t)base + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
+                        plane_copy_board(puzzles + q * 81, sols + q * 81, lane);
+                        if (lane == 0) status[q] = ((bad >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
+                    }
+                    if (state == PL_CANCELLED) state = PL_IDLE;
+#if SDK_PLANE_STAMPS
+                    st_dep += __builtin_amdgcn_s_memtime() - st_r2;
+#endif
                 }
-                if (loaded) state = PL_ACTIVE;
             }
             // ---- tail: the queue is empty and the wave is down to a few
             // boards.  A pass costs the whole wave whatever its active
@@ -635,6 +684,10 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 if (rdlane(leave, 0)) break;
             }
         }
+#if SDK_PLANE_STAMPS
+        st_tb = __builtin_amdgcn_s_memtime();
+        st_io += st_tb - st_ta;
+#endif
         if (state != PL_ACTIVE) continue;
 
         // ---- one pass of this lane's board
@@ -689,6 +742,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             }
         }
     }
+#if SDK_PLANE_STAMPS
+    const uint64_t st_tt = __builtin_amdgcn_s_memtime();
+#endif
     if (tail_act) {
         // after the loop: the planes are dead, the wave solver gets the registers
         uint32_t wst[3];
@@ -702,12 +758,20 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     }
 #if SDK_PLANE_STAMPS
     {
-        int64_t *st = defer_list + (PLANE_DEFER_CAP / 2) + 4 * (g >> 6);
+        st_tail = __builtin_amdgcn_s_memtime() - st_tt;
+        int64_t *st = defer_list + (PLANE_DEFER_CAP / 2) + 16 * (g >> 6);
         const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) st[0] = (int64_t)st_t0;
         if (lane == 1) st[1] = (int64_t)(st_t1 ? st_t1 : t2);
         if (lane == 2) st[2] = (int64_t)t2;
         if (lane == 3) st[3] = (int64_t)st_after;
+        if (lane == 4) st[4] = (int64_t)st_pass;
+        if (lane == 5) st[5] = (int64_t)st_io;
+        if (lane == 6) st[6] = (int64_t)st_tail;
+        if (lane == 7) st[7] = (int64_t)st_iters;
+        if (lane == 8) st[8] = (int64_t)st_atom;
+        if (lane == 9) st[9] = (int64_t)st_dma;
+        if (lane == 10) st[10] = (int64_t)st_dep;
     }
 #endif
     // per-wave statistics: the lanes' counts summed, one atomic per counter and wave
