@@ -1,7 +1,7 @@
 """Per-wave timeline of one plane_kernel launch (diagnostic build with
 SDK_PLANE_STAMPS=1, loaded with SDK_LIB=...libsudoku_hip_stamps.so).
 
-    SDK_LIB=$PWD/sudoku_solver_distributed_amd/libsudoku_hip_stamps.so python scripts/plane_timeline.py [BATCH]
+    SDK_LIB=$PWD/sudoku_solver_distributed_amd/libsudoku_hip_stamps.so python scripts/plane_timeline.py [BATCH [hard_search]]
 
 Prints, in microseconds from the first wave's start: when waves saw the
 queue drained and when they exited (percentiles over waves), and the loop
@@ -13,13 +13,14 @@ import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
-from sudoku_solver_distributed_amd.gen import hard17_batch  # noqa: E402
+from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch  # noqa: E402
 from sudoku_solver_distributed_amd.solver import get_solver  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 solver = get_solver("cuda:0")
 lib = solver.lib
-boards = hard17_batch(n, seed=2024, device="cuda:0")
+make = hard_search_batch if (len(sys.argv) > 2 and sys.argv[2] == "hard_search") else hard17_batch
+boards = make(n, seed=2024, device="cuda:0")
 for _ in range(3):
     solver.solve(boards)
 torch.cuda.synchronize()
