@@ -45,6 +45,7 @@ life = (st[:, 2] - st[:, 0]) / 100.0
 cyc = st[:, 4] + st[:, 5] + st[:, 6]
 print(f"wave lifetime us: mean {life.mean():.1f}; loop iterations: mean {st[:, 7].mean():.1f}")
 for k, name in ((4, "pass"), (5, "store+refill+control"), (8, "  of which queue atomic"), (9, "  of which span DMA"),
-                (10, "  of which deposit"), (6, "tail restarts")):
+                (10, "  of which deposit"), (11, "  of which store"),
+                (6, "tail (wide / restart)")):
     print(f"  {name:22s} {st[:, k].sum() / cyc.sum():.3f} of stamped cycles, {st[:, k].mean() / 1e3:.1f} kcycles per wave")
 print(f"  stamped kcycles per wave {cyc.mean() / 1e3:.1f} (shader clock; lifetime {life.mean():.1f} us)")

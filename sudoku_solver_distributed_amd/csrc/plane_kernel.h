@@ -1,47 +1,47 @@
-// plane_kernel.h -- v5 solve kernel: one board per LANE on digit planes
-// (plane_solver.h), included by sudoku_kernels.hip after the packed kernel.
+// plane_kernel.h -- the hot solve kernel: one board per LANE on digit planes
+// (plane_solver.h), built in its own translation unit (plane_kernels.hip).
 //
-// Why a lane per board: the wave-per-board kernels spend ~1650 wave
-// instructions per hard board (29 sweeps x ~57), most of them masks for 81
-// cells spread over 64 lanes, LDS round trips and wave-uniform control.  On
-// digit planes one lane runs a whole pass over its board in ~1800 lane
-// instructions, i.e. ~28 wave instructions per board-pass, and a pass does
-// naked AND hidden singles for all cells (19 passes per hard board instead
-// of 29 sweeps).
+// Why a lane per board: on digit planes one lane runs a whole propagation
+// pass over its board (naked AND hidden singles for every cell and unit) in
+// ~1300 issue slots, i.e. ~20 wave instructions per board-pass, where a
+// wave-per-board solver spends ~57 per sweep on masks for 81 cells spread
+// over 64 lanes, LDS round trips and wave-uniform control.
 //
 // Execution: persistent lanes.  Each lane holds one board (27 plane words +
 // 3 bookkeeping words in VGPRs) and steps it one pass per loop iteration;
-// guesses push the 27 words to a per-lane stack in the caller's workspace
-// ([level][word][lane]: one level's words of the 64 lanes of a wave are
-// contiguous).  Finished lanes wait until at least SDK_PLANE_REFILL lanes of
-// the wave are free, then stores and refills run once for all of them: the
-// 81-byte load and store code is lane-divergent, so running it every
-// iteration for one lane would cost the whole wave.  Boards come from one
-// atomic queue head per wave refill.
+// guesses push the 27 words + the branch entry to the lane's stack lines in
+// the workspace (PlaneStack).  Finished lanes wait until at least
+// SDK_PLANE_REFILL lanes of the wave are free, then stores and refills run
+// once for all of them (the 81-byte I/O is wave-cooperative).  Boards come
+// from a static first hand-out and then chunked claims on one queue head.
+//
+// Once the queue is empty, a wave down to SDK_PLANE_TAIL boards hands them to
+// the wave-wide solver (plane_wide.h): each board in turn is spread over the
+// whole wave and its search continues from the lane's state and stack.
 //
 // Boards the planes cannot take -- givens that repeat a digit in a unit
 // (rules B/C are unsound there, plane_solver.h; tested only once a board's
 // search ends without a completion, since a completion proves the givens
 // clean) or a search deeper than PLANE_MAX_DEPTH -- get status SDK_DEFERRED
-// and no output; the packed
-// kernel then runs over the batch with deferred_only set and solves exactly
-// those.  Results are identical either way.
+// and an entry in the deferred list; solvep_deferred_kernel solves exactly
+// those afterwards.  Results are identical either way.
 #ifndef SDK_PLANE_KERNEL_H
 #define SDK_PLANE_KERNEL_H
 
 #include "plane_solver.h"
 #include "packed_solver.h"
+#include "plane_wide.h"
 
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
-// $SDK_PLANE_TAIL, $SDK_PLANE_DONATE)
+// $SDK_PLANE_TAIL, $SDK_PLANE_TAIL_MODE, $SDK_PLANE_CHUNK)
 #ifndef SDK_PLANE_REFILL
 #define SDK_PLANE_REFILL 12
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 2
+#define SDK_PLANE_TAIL 16
 #endif
-#ifndef SDK_PLANE_DONATE
-#define SDK_PLANE_DONATE 0
+#ifndef SDK_PLANE_TAIL_MODE
+#define SDK_PLANE_TAIL_MODE 1  // 1: continue on the wave-wide solver, 0: restart on the wave-per-board solver
 #endif
 #ifndef SDK_PLANE_CHUNK
 #define SDK_PLANE_CHUNK 64
@@ -249,36 +249,111 @@ __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__
     return shift;
 }
 
-// ---- drain mailbox (one per workgroup, LDS; SDK_PLANE_DONATE > 0)
-// Once the queue is empty a pass still costs a wave the same whatever its
-// active lanes.  A drained wave down to `donate` boards or fewer offers them
-// to its workgroup's other waves -- only when their published idle lanes can
-// take them at once -- and exits; drained waves take offered boards into
-// idle lanes at every iteration.  A board travels as its 27 plane words,
-// index, depth, guess count and stack SLOT (stacks are addressed by slot, so
-// the stack does not move).  The block's last live wave never offers.
-enum { MB_CAP = 64, MB_WORDS = 32 };  // record: 27 planes, p lo / hi, depth, slot offset, guesses
-struct PlaneMailbox {
-    uint32_t w[MB_WORDS][MB_CAP];  // record r's word k at w[k][r]
-    uint32_t lock, count, live, pad;
-    uint32_t idle[PLANE_THREADS / 64];  // idle lanes each drained wave can take (0 otherwise)
-};
-
-// lane 0 only
-__device__ __forceinline__ void mb_lock(PlaneMailbox &mb)
-{
-    while (atomicCAS(&mb.lock, 0u, 1u) != 0u) __builtin_amdgcn_s_sleep(1);
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
-}
-__device__ __forceinline__ void mb_unlock(PlaneMailbox &mb)
-{
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
-    atomicExch(&mb.lock, 0u);
-}
 // lanes of `mask` below this lane
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// ---- the wave-wide tail (plane_wide.h)
+// a record per handed-over board in the wave's staging area (stride: odd, so
+// 64 lanes writing one word each hit 64 banks): 27 plane words, board index
+// lo / hi, depth, stack line offset, guesses so far
+enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = PLANE_STAGE_DWORDS / PLANE_TAIL_REC - 1 };
+
+// The board's stack in the wide layout: lane 16b+d owns word 3d+b of each
+// level's line; the branch entry (word 27) goes through lane 48 (a pad lane)
+// on a push, lane 0 on an update; every lane reads it.
+struct WideStack {
+    __amdgpu_buffer_rsrc_t rsrc;
+    uint32_t lane_off;  // the board's stack (uniform)
+    uint32_t off;       // this lane's word: 4 * (3d + b); pad lanes the entry (108)
+    bool valid, entry_lane;
+    __device__ __forceinline__ void push(uint32_t level, uint32_t w, const wide::Lanes &, uint32_t entry) const
+    {
+        if (valid || entry_lane)
+            __builtin_amdgcn_raw_buffer_store_b32(valid ? w : entry, rsrc, (int)(lane_off + level * 128u + off), 0, 0);
+    }
+    __device__ __forceinline__ uint32_t entry(uint32_t level) const
+    {
+        return __builtin_amdgcn_readfirstlane(
+            __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + level * 128u + 108u), 0, 0));
+    }
+    __device__ __forceinline__ uint32_t restore(uint32_t level, const wide::Lanes &) const
+    {
+        const uint32_t x = __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + level * 128u + off), 0, 0);
+        return valid ? x : 0u;
+    }
+    __device__ __forceinline__ void put_entry(uint32_t level, uint32_t e) const
+    {
+        if (__lane_id() == 0) __builtin_amdgcn_raw_buffer_store_b32(e, rsrc, (int)(lane_off + level * 128u + 108u), 0, 0);
+    }
+};
+
+// Solve the k boards recorded in `recs` on the wave-wide solver, one after
+// the other.  st: solved, guesses (net of deferred boards'), passes,
+// deferred -- wave-uniform.
+__device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
+                                             const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols,
+                                             int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+                                             int64_t *__restrict__ defer_list, const int64_t *best, int node_order,
+                                             uint32_t (&st)[5])
+{
+    const wide::Lanes L = wide::lanes();
+    const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
+    const uint32_t pos = (uint32_t)lane & 31u, a0 = ((uint32_t)lane >> 5) << 6;  // store: slot 0's band row
+    uint32_t solved = 0, guesses = 0, passes = 0, deferred = 0;
+    for (int s = 0; s < k; ++s) {
+        const uint32_t *rec = recs + PLANE_TAIL_REC * s;
+        uint32_t w = rec[L.valid ? L.word : 0u];
+        w = L.valid ? w : 0u;
+        const int64_t pb = ((int64_t)__builtin_amdgcn_readfirstlane(rec[28]) << 32) |
+                           (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(rec[27]);
+        uint32_t depth = __builtin_amdgcn_readfirstlane(rec[29]);
+        const WideStack stk = {stack_rsrc, (uint32_t)__builtin_amdgcn_readfirstlane(rec[30]),
+                               L.valid ? 4u * L.word : 108u, L.valid, lane == 48};
+        wide::Stats ws_ = {0u, 0u, (uint32_t)__builtin_amdgcn_readfirstlane(rec[31])};
+        const int r = wide::solve(w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_, [&] {
+            return best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pb;
+        });
+        passes += ws_.passes;
+        guesses += ws_.guesses;
+        const uint8_t *src = puzzles + pb * 81;
+        uint8_t *dst = sols + pb * 81;
+        if (r == wide::W_SOLVED) {
+            uint32_t sl[4];
+            wide::value_slices(w, L, sl);
+            uint32_t v0 = 0, v1 = 0;
+#pragma unroll
+            for (int b = 0; b < 4; ++b) {
+                v0 |= ((wide::bperm(sl[b], a0) >> pos) & 1u) << b;
+                v1 |= ((wide::rdl(sl[b], 32) >> pos) & 1u) << b;
+            }
+            if (c0 >= 0) dst[c0] = (uint8_t)v0;
+            if (c1 >= 0) dst[c1] = (uint8_t)v1;
+            if (lane == 0) {
+                status[pb] = SDK_SOLVED;
+                if (best) __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            solved++;
+        } else if (r == wide::W_CANCELLED) {
+            plane_copy_board(src, dst, lane);
+            if (lane == 0) status[pb] = SDK_CANCELLED;
+        } else if (r == wide::W_OVERFLOW || plane_givens_clash(src, c0, c1)) {
+            // too deep for the stack, or no completion on clashing givens
+            // (rules B/C unsound): the wave kernel's
+            if (lane == 0) plane_defer(pb, status, ws, defer_list);
+            deferred++;
+            guesses -= ws_.bguess;
+        } else {
+            plane_copy_board(src, dst, lane);
+            if (lane == 0) status[pb] = SDK_UNSOLVABLE;
+        }
+    }
+    st[0] = solved;
+    st[1] = guesses;
+    st[2] = passes;
+    st[3] = deferred;
 }
 
 // lane states; the two "original" states store the input board back
@@ -303,20 +378,9 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int donate, int chunk)
+    int order, int refill, int tail, int tail_mode, int chunk)
 {
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
-    __shared__ PlaneMailbox mb;
-    const int wid = threadIdx.x >> 6;
-    if (donate > 0) {
-        if (threadIdx.x < PLANE_THREADS / 64) mb.idle[threadIdx.x] = 0;
-        if (threadIdx.x == 0) {
-            mb.lock = 0;
-            mb.count = 0;
-            mb.live = PLANE_THREADS / 64;
-        }
-        __syncthreads();
-    }
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     const uint8_t *stage_b = (const uint8_t *)stage;
@@ -358,6 +422,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // the tail restarts (s_memtime at wave-uniform points)
     uint64_t st_pass = 0, st_io = 0, st_tail = 0, st_tb = 0;
     uint64_t st_atom = 0, st_dma = 0, st_dep = 0;  // parts of st_io: queue atomic, span DMA, per-board deposit
+    uint64_t st_store = 0;                          // part of st_io: storing finished boards
 #endif
 
     // Start-up: the wave's first 64 boards arrive as one staged span; each
@@ -405,36 +470,6 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             st_after++;
         }
 #endif
-        if (drained && donate > 0) {
-            // ---- drain mailbox: publish idle lanes, take offered boards
-            const uint64_t idle = __builtin_amdgcn_ballot_w64(state == PL_IDLE);
-            if (lane == 0) mb.idle[wid] = (uint32_t)__builtin_popcountll(idle);
-            if (idle && __hip_atomic_load(&mb.count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) {
-                uint32_t base = 0, take = 0;
-                if (lane == 0) {
-                    mb_lock(mb);
-                    const uint32_t c = mb.count, ni = (uint32_t)__builtin_popcountll(idle);
-                    take = c < ni ? c : ni;
-                    base = c - take;
-                    mb.count = base;
-                }
-                take = rdlane(take, 0);
-                const uint32_t rk = lanes_below(idle);
-                if (state == PL_IDLE && rk < take) {
-                    const uint32_t r = rdlane(base, 0) + rk;
-#pragma unroll
-                    for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = mb.w[w][r];
-                    B.Det[0] = B.Det[1] = B.Det[2] = 0;
-                    p = (int64_t)(((uint64_t)mb.w[28][r] << 32) | mb.w[27][r]);
-                    depth = mb.w[29][r];
-                    stk.lane_off = mb.w[30][r];
-                    bguess = mb.w[31][r];
-                    guesses += bguess;
-                    state = PL_ACTIVE;
-                }
-                if (lane == 0) mb_unlock(mb);
-            }
-        }
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
         if (__builtin_popcountll(~active) >= refill || active == 0) {
             const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
@@ -443,6 +478,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // 12 words) to the LDS staging area, all lanes at once; then the
             // wave stores one board at a time, each lane reading the slices
             // of its two cells' bands (same words for every lane: broadcast).
+#if SDK_PLANE_STAMPS
+            const uint64_t st_s0 = __builtin_amdgcn_s_memtime();
+#endif
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
             solved += state == PL_SOLVED;
             if (m) {
@@ -509,6 +547,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // cell) and v_writelane drops the 12 slice words into the
             // board's lane, into plane words the idle lane does not use;
             // finally every loaded lane turns its slices into planes at once
+#if SDK_PLANE_STAMPS
+            st_store += __builtin_amdgcn_s_memtime() - st_s0;
+#endif
             if (!drained) {
                 const uint64_t idle = ~active;
                 const int k = __builtin_popcountll(idle);
@@ -606,83 +647,19 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             // ---- tail: the queue is empty and the wave is down to a few
             // boards.  A pass costs the whole wave whatever its active
             // lanes, so the wave would idle on its slowest board for tens of
-            // passes; instead it restarts each of them on the wave-per-board
-            // solver (packed_solver.h, ~one pass's worth of instructions per
-            // board) and exits.
+            // passes; instead it hands them, one at a time, to the wave-wide
+            // solver (plane_wide.h: the search continues, ~150 instructions
+            // per pass) -- or, tail_mode 0, restarts each of them on the
+            // wave-per-board solver (packed_solver.h) -- and exits.
             if (drained && tail > 0) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                uint32_t go = act && __builtin_popcountll(act) <= tail;
-                if (go && donate > 0) {
-                    // with the mailbox on, only the block's last live wave, and only
-                    // with nothing offered (a sibling may have just offered boards)
-                    if (lane == 0) {
-                        mb_lock(mb);
-                        go = mb.live == 1 && mb.count == 0;
-                        if (go) mb.live = 0;
-                        mb_unlock(mb);
-                    }
-                    go = rdlane(go, 0);
-                }
-                if (go) {
-                    if (state == PL_ACTIVE) guesses -= bguess;  // those searches start over
+                if (act && __builtin_popcountll(act) <= tail) {
+                    if (state == PL_ACTIVE && !tail_mode) guesses -= bguess;  // those searches start over
                     tail_act = act;
                     break;
                 }
             }
-            if (drained && donate > 0) {
-                // ---- offer this wave's boards if the others can take them now
-                const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                const uint32_t na = (uint32_t)__builtin_popcountll(act);
-                if (na > 0 && na <= (uint32_t)donate) {
-                    uint32_t ok = 0, base = 0;
-                    if (lane == 0) {
-                        mb_lock(mb);
-                        uint32_t room = 0;
-#pragma unroll
-                        for (int w = 0; w < PLANE_THREADS / 64; ++w) room += w == wid ? 0u : mb.idle[w];
-                        if (mb.live > 1 && mb.count + na <= room && mb.count + na <= (uint32_t)MB_CAP) {
-                            base = mb.count;
-                            mb.count = base + na;
-                            mb.live -= 1;
-                            mb.idle[wid] = 0;
-                            ok = 1;
-                        } else {
-                            mb_unlock(mb);
-                        }
-                    }
-                    if (rdlane(ok, 0)) {
-                        if (state == PL_ACTIVE) {
-                            const uint32_t r = rdlane(base, 0) + lanes_below(act);
-#pragma unroll
-                            for (int w = 0; w < 27; ++w) mb.w[w][r] = B.P[w / 3][w % 3];
-                            mb.w[27][r] = (uint32_t)p;
-                            mb.w[28][r] = (uint32_t)(p >> 32);
-                            mb.w[29][r] = depth;
-                            mb.w[30][r] = stk.lane_off;
-                            mb.w[31][r] = bguess;
-                            guesses -= bguess;  // counted by the wave that finishes it
-                            state = PL_IDLE;
-                        }
-                        if (lane == 0) mb_unlock(mb);
-                        break;
-                    }
-                }
-            }
-            if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) {
-                // nothing left here: leave, unless boards wait in the mailbox
-                uint32_t leave = 1;
-                if (donate > 0 && lane == 0) {
-                    mb_lock(mb);
-                    if (mb.count == 0) {
-                        mb.live -= 1;
-                        mb.idle[wid] = 0;
-                    } else {
-                        leave = 0;
-                    }
-                    mb_unlock(mb);
-                }
-                if (rdlane(leave, 0)) break;
-            }
+            if (drained && __builtin_amdgcn_ballot_w64(state != PL_IDLE) == 0) break;  // nothing left here
         }
 #if SDK_PLANE_STAMPS
         st_tb = __builtin_amdgcn_s_memtime();
@@ -745,7 +722,34 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
 #endif
-    if (tail_act) {
+    if (tail_act && tail_mode) {
+        // ---- wave-wide tail: the lanes' boards go to LDS records (27 plane
+        // words, index, depth, stack line, guesses; stride 33 dwords, so the
+        // lanes' writes and a record's reads are conflict-free) and the wave
+        // continues each search in turn on the wide solver
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the lanes' stack pushes have landed
+        if ((tail_act >> lane) & 1u) {
+            uint32_t *rec = stage + PLANE_TAIL_REC * lanes_below(tail_act);
+#pragma unroll
+            for (int w = 0; w < 27; ++w) rec[w] = B.P[w / 3][w % 3];
+            rec[27] = (uint32_t)p;
+            rec[28] = (uint32_t)(p >> 32);
+            rec[29] = depth;
+            rec[30] = stk.lane_off;
+            rec[31] = bguess;
+        }
+        wave_lds_sync();
+        uint32_t wst[5];
+        plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, puzzles, sols, status, ws, defer_list,
+                        best, node_order, wst);
+        if (lane == 0) {
+            solved += wst[0];
+            guesses += wst[1];
+            passes += wst[2];
+            fin -= wst[3];
+            deferred += wst[3];
+        }
+    } else if (tail_act) {
         // after the loop: the planes are dead, the wave solver gets the registers
         uint32_t wst[3];
         plane_tail(tail_lds[threadIdx.x >> 6], lane, tail_act, (uint32_t)p, (uint32_t)(p >> 32), puzzles, sols,
@@ -772,6 +776,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         if (lane == 8) st[8] = (int64_t)st_atom;
         if (lane == 9) st[9] = (int64_t)st_dma;
         if (lane == 10) st[10] = (int64_t)st_dep;
+        if (lane == 11) st[11] = (int64_t)st_store;
     }
 #endif
     // per-wave statistics: the lanes' counts summed, one atomic per counter and wave

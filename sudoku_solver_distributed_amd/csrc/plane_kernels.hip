@@ -10,9 +10,9 @@
 
 // runtime tuning knobs (A/B without a rebuild): $SDK_PLANE_REFILL idle lanes
 // before a wave refills, $SDK_PLANE_TAIL active lanes at or below which a
-// wave restarts its last boards on the wave-per-board solver once the queue
-// is empty (0: off), $SDK_PLANE_DONATE active lanes at or below which a
-// drained wave offers its boards to its workgroup's other waves (0: off),
+// drained wave hands its last boards to the tail solver (0: off; at most
+// PLANE_TAIL_MAX), $SDK_PLANE_TAIL_MODE that solver (1: the wave-wide solver
+// continues each search, 0: the wave-per-board solver restarts it),
 // $SDK_PLANE_CHUNK most boards a wave claims from the queue at once (0: one
 // claim per refill)
 static int env_int(const char *name, int dflt)
@@ -26,12 +26,13 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
                             int64_t threads, hipStream_t st)
 {
     static const int refill = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
-    static const int tail = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
-    static const int donate = env_int("SDK_PLANE_DONATE", SDK_PLANE_DONATE);
+    static const int tail_env = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
+    static const int tail = tail_env > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail_env;
+    static const int tail_mode = env_int("SDK_PLANE_TAIL_MODE", SDK_PLANE_TAIL_MODE);
     static const int chunk = env_int("SDK_PLANE_CHUNK", SDK_PLANE_CHUNK);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, defer_list, ordered, order, refill, tail, donate, chunk);
+                       stack, defer_list, ordered, order, refill, tail, tail_mode, chunk);
     return hipGetLastError();
 }
 

@@ -137,3 +137,91 @@ def test_pass_matches_previous_formulation(host):
                                                   hard_search_batch(300, seed=12).numpy(),
                                                   grids]))
     assert host.plane_check_pass(boards.ctypes.data, len(boards), 200_000, 99) == 0
+
+
+# ---- the wave-wide tail solver (csrc/plane_wide.h) over an emulated wave
+
+@pytest.fixture(scope="module")
+def wide(tmp_path_factory):
+    out = os.path.join(str(tmp_path_factory.mktemp("wide")), "libwide_host.so")
+    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-o", out,
+                           os.path.join(NATIVE, "wide_host.cpp")])
+    lib = ctypes.CDLL(out)
+    lib.wide_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                     ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]
+    lib.wide_check_fixpoint.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
+    lib.wide_check_fixpoint.restype = ctypes.c_int64
+    return lib
+
+
+def _wide(lib, boards, node_order=0, lane_guesses=0, max_depth=81, stats=None):
+    boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
+    out = np.zeros_like(boards)
+    st = np.zeros(len(boards), dtype=np.int32)
+    g, pl, pw = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    lib.wide_solve_batch(boards.ctypes.data, out.ctypes.data, st.ctypes.data, len(boards), node_order,
+                         max_depth, lane_guesses, ctypes.byref(g), ctypes.byref(pl), ctypes.byref(pw))
+    if stats is not None:
+        stats.update(guesses=g.value, passes_lane=pl.value, passes_wide=pw.value)
+    return out, st
+
+
+def _mixed_boards(n=150, seed=21):
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    grids, _ = O.solve_unique_batch(hard17_batch(n, seed=seed).numpy())
+    rng = np.random.default_rng(seed)
+    for g in grids:
+        g[rng.choice(81, 56, replace=False)] = 0
+    return np.ascontiguousarray(np.concatenate([hard17_batch(n, seed=seed + 1).numpy(),
+                                                hard_search_batch(n, seed=seed + 2).numpy(), grids,
+                                                np.zeros((1, 81), np.uint8)]))
+
+
+def test_wide_fixpoint_matches_lane_pass(wide):
+    """Jacobi hidden singles over the wave reach the lane pass's fixpoint
+    (same verdict, same planes, same undetermined cells), from each board and
+    from 20 random mid-search states per board; the only admitted
+    disagreements are states holding two determined cells with one digit in
+    a unit (wide_host.cpp wide_check_fixpoint)."""
+    boards = _mixed_boards()
+    assert wide.wide_check_fixpoint(boards.ctypes.data, len(boards), 20, 5) == 0
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+@pytest.mark.parametrize("lane_guesses", [0, 1, 3])
+def test_wide_continuation_vs_lane_solver(host, wide, order, lane_guesses):
+    """Hand a board from the lane solver to the wave-wide solver after
+    `lane_guesses` guesses (0: the whole search wide): identical answers and
+    statuses.  The wide pass eliminates this pass's hidden singles at once,
+    so it meets contradictions (a duplicated determined digit) no later than
+    the lane pass: never more guesses, up to 1 % noise."""
+    boards = _mixed_boards()
+    no = int(order == "node")
+    s_lane, s_wide = {}, {}
+    want, wst = _solve(host, boards, node_order=no, stats=s_lane)
+    got, gst = _wide(wide, boards, node_order=no, lane_guesses=lane_guesses, stats=s_wide)
+    assert np.array_equal(gst, wst)
+    assert np.array_equal(got, want)
+    assert s_wide["guesses"] <= 1.01 * s_lane["guesses"]
+    if lane_guesses == 0:
+        assert s_wide["passes_wide"] > 0 and s_wide["passes_lane"] == 0
+
+
+def test_wide_edge_cases(wide):
+    full = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
+    boards = np.array([b81(x) for x in (full, "0" * 81, full[:40] + "0" + full[41:])], dtype=np.uint8)
+    got, st = _wide(wide, boards)
+    want, wst = O.solve_batch(boards, order="gen")
+    assert np.array_equal(st, wst) and np.array_equal(got, want)
+    # an unsolvable board: cell (8, 8) has no candidate (row 8 holds 2..9,
+    # column 8 a 1); the gen.py walk starts there, so the oracle ends at once
+    dead = np.zeros((1, 81), np.uint8)
+    dead[0, 72:80] = [2, 3, 4, 5, 6, 7, 8, 9]
+    dead[0, 63 + 8] = 1
+    got, st = _wide(wide, dead)
+    want, wst = O.solve_batch(dead, order="gen")
+    assert st[0] == wst[0] == 0 and np.array_equal(got, want)
+    # depth overflow hands the board on
+    _, st = _wide(wide, np.zeros((1, 81), np.uint8), max_depth=3)
+    assert st[0] == 2
