@@ -38,7 +38,7 @@
 #define SDK_PLANE_REFILL 12
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 16
+#define SDK_PLANE_TAIL 8
 #endif
 #ifndef SDK_PLANE_TAIL_MODE
 #define SDK_PLANE_TAIL_MODE 1  // 1: continue on the wave-wide solver, 0: restart on the wave-per-board solver
@@ -220,6 +220,8 @@ __device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, u
 enum { PLANE_STAGE_DWORDS = 1348, PLANE_STAGE_ZERO = 4 * (PLANE_STAGE_DWORDS - 1) };
 
 typedef __attribute__((address_space(3))) void lds_void_t;
+// s_waitcnt immediates (gfx9: vmcnt bits 3:0 + 15:14, expcnt 6:4, lgkmcnt 11:8)
+enum { SDK_WAIT_VM0 = 0x0F70, SDK_WAIT_LGKM0 = 0xC07F, SDK_WAIT_VM0_LGKM0 = 0x0070 };
 
 __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__ puzzles, int64_t n, int64_t q0, int k,
                                                      uint32_t *stage, int lane)
@@ -234,17 +236,20 @@ __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__
     // the DMA writes LDS through the memory path, unordered with this wave's
     // earlier ds_writes to the same area (the store path's bit-slices):
     // those must have landed first
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_waitcnt(SDK_WAIT_LGKM0);
     for (uint32_t i = 0; i < nd; i += 64)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(rsrc, (lds_void_t *)(stage + i), 4, (int)((i + lane) * 4u), 0, 0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // (the builtin, not inline asm: the compiler's wait tracking sees it, so
+    // later LDS reads do not wait on every outstanding store "in case" they
+    // alias the DMA -- with asm here the store loop drained vmcnt per board)
+    __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);
     // the batch's last dword may be partial: the range check zeroes all of
     // it, so its bytes come in one by one
     const uint64_t tail = total & ~3ull;
     if ((total & 3u) && tail >= a0 && tail < a0 + 4ull * nd) {
         uint8_t *sb = (uint8_t *)stage;
         if ((uint64_t)lane < (total & 3u)) sb[tail - a0 + lane] = puzzles[tail + lane];
-        asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0_LGKM0);
     }
     return shift;
 }
@@ -499,12 +504,16 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     }
                 }
                 const uint32_t pos = lane & 31, b0 = (uint32_t)lane >> 5;  // slot 0: band 0 / 1, slot 1: band 2
-                while (m) {
-                    const int i = __builtin_ctzll(m);
-                    m &= m - 1;
+                // software-pipelined: board i's records are read while the
+                // previous board's bytes go out
+                int i = __builtin_ctzll(m);
+                sdk_v4u t0 = stage4[b0 * 64 + i], t1 = stage4[2 * 64 + i];
+                for (;;) {
                     const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
+                    m &= m - 1;
+                    const int in = m ? __builtin_ctzll(m) : i;
+                    const sdk_v4u n0 = stage4[b0 * 64 + in], n1 = stage4[2 * 64 + in];
                     uint8_t *dst = sols + pi * 81;
-                    const sdk_v4u t0 = stage4[b0 * 64 + i], t1 = stage4[2 * 64 + i];
                     // value = bit k of (slice k << k) >> pos, k = 0..3
                     const uint32_t v0 = plane::sel(7u, plane::sel(3u, plane::sel(1u, t0.x >> pos, t0.y >> pos), t0.z >> pos),
                                                    t0.w >> pos) & 15u;
@@ -512,8 +521,12 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                                                    t1.w >> pos) & 15u;
                     if (c0 >= 0) dst[c0] = (uint8_t)v0;
                     if (c1 >= 0) dst[c1] = (uint8_t)v1;
-                    if (lane == 0) status[pi] = SDK_SOLVED;
+                    if (!m) break;
+                    i = in;
+                    t0 = n0;
+                    t1 = n1;
                 }
+                if (state == PL_SOLVED) status[p] = SDK_SOLVED;  // every solved lane its own, one store
             }
             // ---- unsolvable / cancelled: the input board back
             m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
@@ -590,12 +603,16 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     const uint32_t st0 = c0 >= 0 ? 81u : 0u, st1 = c1x >= 0 ? 81u : 0u;
                     const uint32_t mlo = lane < 32 ? 1u : 2u, mhi = lane < 32 ? 4u : 8u;
                     uint64_t mm = idle, loaded = 0, bad = 0;
+                    // software-pipelined: the next board's bytes are read
+                    // while this board's ballots run (reads past the span
+                    // stay inside the staging area and are never used)
+                    uint32_t a0 = stage_b[ad0], a1 = stage_b[ad1];
                     for (int j = 0; j < kk; ++j) {
                         const int i = __builtin_ctzll(mm);
                         mm &= mm - 1;
-                        const uint32_t a0 = stage_b[ad0], a1 = stage_b[ad1];
                         ad0 += st0;
                         ad1 += st1;
+                        const uint32_t n0 = stage_b[ad0], n1 = stage_b[ad1];
                         const uint64_t s0 = __builtin_amdgcn_ballot_w64((a0 & 1u) != 0u);
                         const uint64_t s1 = __builtin_amdgcn_ballot_w64((a0 & 2u) != 0u);
                         const uint64_t s2 = __builtin_amdgcn_ballot_w64((a0 & 4u) != 0u);
@@ -610,6 +627,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                         PLANE_DROP(2, 0, s2); PLANE_DROP(2, 1, s2 >> 32); PLANE_DROP(2, 2, u23);
                         PLANE_DROP(3, 0, s3); PLANE_DROP(3, 1, s3 >> 32); PLANE_DROP(3, 2, u23 >> 32);
 #undef PLANE_DROP
+                        a0 = n0;
+                        a1 = n1;
                     }
                     if ((loaded >> lane) & 1u) {
                         fin++;
@@ -727,7 +746,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         // words, index, depth, stack line, guesses; stride 33 dwords, so the
         // lanes' writes and a record's reads are conflict-free) and the wave
         // continues each search in turn on the wide solver
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the lanes' stack pushes have landed
+        __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // the lanes' stack pushes have landed
         if ((tail_act >> lane) & 1u) {
             uint32_t *rec = stage + PLANE_TAIL_REC * lanes_below(tail_act);
 #pragma unroll
