@@ -127,6 +127,17 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
 #define SDK_KERNEL_PLANE 6
 int sdk_set_solve_kernel(int kernel);
 
+/* Plane-kernel tuning (library extension, no reference counterpart; the
+ * defaults are the measured optimum).  refill: idle lanes
+ * before a wave refills; tail: active lanes at or below which a drained wave
+ * hands its last boards to the tail solver (0 off, at most 40); tail_mode: 1
+ * the wave-wide solver continues each search, 0 the wave-per-board solver
+ * restarts it; chunk: most boards a wave claims from the queue at once.  A
+ * negative value keeps that knob; all four negative restore the defaults
+ * ($SDK_PLANE_REFILL / _TAIL / _TAIL_MODE / _CHUNK).  Results never depend on
+ * them.  Returns 0, or -1 for an out-of-range value (nothing changed). */
+int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk);
+
 /* Library / device info. */
 const char *sdk_last_error(void);
 const char *sdk_version(void);

@@ -35,6 +35,7 @@ EXPORTS = (
     "sdk_version",
     "sdk_device_cu_count",
     "sdk_set_solve_kernel",
+    "sdk_set_plane_tuning",
 )
 SDK_KERNELS = {"auto": 1, "packed": 5, "plane": 6}
 # device symbol of each solve kernel (rocprofv3 Kernel_Name, profiles/pmc_<symbol>.json)
@@ -80,6 +81,8 @@ def load() -> ctypes.CDLL:
     L.sdk_device_cu_count.argtypes = []
     L.sdk_set_solve_kernel.restype = i32
     L.sdk_set_solve_kernel.argtypes = [i32]
+    L.sdk_set_plane_tuning.restype = i32
+    L.sdk_set_plane_tuning.argtypes = [i32, i32, i32, i32]
     _lib = L
     return L
 

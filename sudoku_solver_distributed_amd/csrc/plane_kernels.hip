@@ -2,8 +2,11 @@
 // solve kernel (plane_kernel.h), built on its own by build.py with LLVM's
 // iterative-ilp machine scheduler (+1.4 % over the default, same registers;
 // $SDK_PLANE_SCHED selects another strategy for A/B builds).  The pass pins its board between digits (plane_solver.h PS_PIN),
-// which keeps it at ~113 VGPRs: four waves per SIMD, no spills.
+// which keeps the kernel at ~120 VGPRs: four waves per SIMD, no spills (forcing
+// five or six waves spills and measured 4 % / 13 % slower).
 #include <stdlib.h>
+
+#include <atomic>
 
 #include "common.h"
 #include "plane_kernel.h"
@@ -21,15 +24,36 @@ static int env_int(const char *name, int dflt)
     return e && e[0] ? atoi(e) : dflt;
 }
 
+// sdk_set_plane_tuning overrides (-1: the environment's / built-in default)
+static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1};
+
+int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
+{
+    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 1 || refill == 0) return -1;
+    if (refill < 0 && tail < 0 && tail_mode < 0 && chunk < 0) {
+        g_refill = g_tail = g_tail_mode = g_chunk = -1;
+        return 0;
+    }
+    if (refill >= 0) g_refill = refill;
+    if (tail >= 0) g_tail = tail;
+    if (tail_mode >= 0) g_tail_mode = tail_mode;
+    if (chunk >= 0) g_chunk = chunk;
+    return 0;
+}
+
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
                             unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
                             int64_t threads, hipStream_t st)
 {
-    static const int refill = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
+    static const int refill_env = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
     static const int tail_env = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
-    static const int tail = tail_env > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail_env;
-    static const int tail_mode = env_int("SDK_PLANE_TAIL_MODE", SDK_PLANE_TAIL_MODE);
-    static const int chunk = env_int("SDK_PLANE_CHUNK", SDK_PLANE_CHUNK);
+    static const int tail_mode_env = env_int("SDK_PLANE_TAIL_MODE", SDK_PLANE_TAIL_MODE);
+    static const int chunk_env = env_int("SDK_PLANE_CHUNK", SDK_PLANE_CHUNK);
+    const int refill = g_refill >= 0 ? g_refill.load() : refill_env;
+    int tail = g_tail >= 0 ? g_tail.load() : tail_env;
+    tail = tail > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail;
+    const int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : tail_mode_env;
+    const int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
                        stack, defer_list, ordered, order, refill, tail, tail_mode, chunk);

@@ -426,3 +426,46 @@ def test_hard_search_4m(solver):
     idx = torch.randint(0, n, (256,), generator=torch.Generator().manual_seed(2))
     want, cnt = O.solve_unique_batch(p[idx.to(p.device)].cpu().numpy())
     assert np.array_equal(sols[idx.to(p.device)].cpu().numpy(), want)
+
+
+@pytest.mark.parametrize("tail,mode", [(40, 1), (40, 0), (0, 1)])
+def test_plane_tail_paths(solver, tail, mode):
+    """The plane kernel's drained-wave tail (sdk_set_plane_tuning): with 40
+    the most boards of every wave end on the tail solver -- wave-wide
+    continuation (mode 1, plane_wide.h) or wave-per-board restart (mode 0);
+    0 switches the tail off.  Search-heavy and hard boards against their
+    unique completion, generated multi-solution boards against the literal
+    walk in both orders, clashing givens (deferred from the tail), an empty
+    board deeper than the stack (deferred), ordered mode."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch, hard_search_batch
+    lib = solver.lib
+    prev = lib.sdk_set_solve_kernel(_lib.SDK_KERNELS["plane"])
+    assert lib.sdk_set_plane_tuning(-1, tail, mode, -1) == 0
+    try:
+        for order in ("gen", "node"):
+            hs = np.concatenate([hard_search_batch(6144, seed=31).numpy(), hard17_batch(2048, seed=32).numpy()])
+            sols, st = solver.solve(torch.from_numpy(hs), order=order)
+            want, cnt = O.solve_unique_batch(hs)
+            assert (cnt == 1).all() and (st.cpu().numpy() == 1).all()
+            assert np.array_equal(sols.cpu().numpy(), want)
+            gen = generate_batch(8192, 50, seed=33).cpu().numpy()
+            gen[:16] = 0  # empty boards: searches deeper than the stack in gen order
+            sols, st = solver.solve(torch.from_numpy(gen), order=order)
+            want, wst = O.solve_batch(gen, order=order)
+            assert np.array_equal(st.cpu().numpy(), wst)
+            assert np.array_equal(sols.cpu().numpy(), want)
+            _duplicate_givens_case(solver, order)
+        # ordered mode: the lowest solvable index wins, later boards solved or cancelled
+        p = hard_search_batch(8192, seed=34)
+        p[:100, :] = torch.tensor(b81("123456780000000009" + "0" * 63), dtype=torch.uint8)  # dead boards
+        sols, st = solver.solve(p, ordered=True)
+        st = st.cpu().numpy()
+        assert (st[:100] == 0).all() and st[100] == 1
+        assert set(np.unique(st[101:])) <= {1, -2}
+        assert solver.stats()["best"] == 100
+        want, _ = O.solve_unique_batch(p[100:101].numpy())
+        assert np.array_equal(sols[100].cpu().numpy(), want[0])
+    finally:
+        lib.sdk_set_plane_tuning(-1, -1, -1, -1)
+        lib.sdk_set_solve_kernel(prev)
