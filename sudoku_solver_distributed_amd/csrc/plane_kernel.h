@@ -264,7 +264,9 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 // a record per handed-over board in the wave's staging area (stride: odd, so
 // 64 lanes writing one word each hit 64 banks): 27 plane words, board index
 // lo / hi, depth, stack line offset, guesses so far
-enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = PLANE_STAGE_DWORDS / PLANE_TAIL_REC - 1 };
+enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = 40 };
+// the last record, read up to word 48 (pad lanes), stays below the zero byte
+static_assert((PLANE_TAIL_MAX - 1) * PLANE_TAIL_REC + 48 < PLANE_STAGE_DWORDS - 1, "tail records");
 
 // The board's stack in the wide layout: lane 16b+d owns word 3d+b of each
 // level's line; the branch entry (word 27) goes through lane 48 (a pad lane)
