@@ -260,6 +260,79 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
 }
 
+// ---- the store path's outbox
+// a record per solved board: value bit-slices V[k][b] (bit 10r + c of band
+// b = bit k of the value at cell (3b + r, c)) and the board index, as
+// V00 V01 V02 V10 | V11 V12 V20 V21 | V22 V30 V31 V32 | p_lo p_hi - -
+enum { PLANE_OUTBOX = 64, PLANE_OB_WORDS = 16 };
+
+// 27 cells of a band word without its guard bits (bit 9r + c)
+__device__ __forceinline__ uint32_t plane_unguard(uint32_t v)
+{
+    return plane::or3(v & 0x1FFu, (v >> 1) & 0x3FE00u, (v >> 2) & 0x7FC0000u);
+}
+
+// Lane j < count writes outbox board j: its 81 bytes as the 21 dwords of its
+// span (sh = the board's offset in its first dword): dwords 1..19 whole, 0
+// and 20 whole when the span starts / ends on a dword boundary, byte by
+// byte otherwise (they hold neighbouring boards' bytes).  Byte expansion:
+// value bit k of 4 consecutive cells, a nibble of the slice's 81-bit cell
+// stream, spreads to bit k of 4 bytes with one multiply (bit i -> bit 8i).
+__device__ __forceinline__ void plane_flush_outbox(const uint32_t *outbox, uint32_t count, int lane,
+                                                   uint8_t *__restrict__ sols)
+{
+    if ((uint32_t)lane < count) {
+        const sdk_v4u *rec = (const sdk_v4u *)(outbox + PLANE_OB_WORDS * lane);
+        const sdk_v4u r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
+        const uint32_t V[4][3] = {{r0.x, r0.y, r0.z}, {r0.w, r1.x, r1.y}, {r1.z, r1.w, r2.x}, {r2.y, r2.z, r2.w}};
+        const int64_t pb = ((int64_t)r3.y << 32) | r3.x;
+        uint8_t *dst = sols + pb * 81;
+        const uint32_t sh = (uint32_t)(uintptr_t)dst & 3u;
+        uint32_t *dw = (uint32_t *)(dst - sh);
+        // per slice: the 81-bit cell stream, shifted up by sh bits (byte
+        // offset sh in the first dword: bit 8i + k of dword j <- cell 4j + i - sh)
+        uint32_t T[4][3];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t w0 = plane_unguard(V[k][0]), w1 = plane_unguard(V[k][1]), w2 = plane_unguard(V[k][2]);
+            const uint32_t s0 = w0 | (w1 << 27), s1 = (w1 >> 5) | (w2 << 22), s2 = w2 >> 10;  // cells 0..80
+            // (x >> 1) >> (31 - sh): the bits carried up, 0 for sh = 0
+            T[k][0] = s0 << sh;
+            T[k][1] = (s1 << sh) | ((s0 >> 1) >> (31u - sh));
+            T[k][2] = (s2 << sh) | ((s1 >> 1) >> (31u - sh));
+        }
+        // dword j of the span from the slices' nibbles 4j..4j+3
+        auto word = [&](const int j) {
+            const int sw = j / 8, sb = (4 * j) % 32;
+            uint32_t acc = 0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t nib = (sb >= k ? (T[k][sw] >> (sb - k)) : (T[k][sw] << (k - sb))) & (0xFu << k);
+                acc |= plane::mul24(nib, 0x204081u) & (0x01010101u << k);
+            }
+            return acc;
+        };
+        // each dword stored as soon as it is made (few live registers)
+#pragma unroll
+        for (int j = 1; j < 20; ++j) dw[j] = word(j);
+        const uint32_t first = word(0), last = word(20);
+        if (sh == 0) {
+            dw[0] = first;
+        } else {
+#pragma unroll
+            for (int i = 1; i < 4; ++i)
+                if ((uint32_t)i >= sh) dst[i - (int)sh] = (uint8_t)(first >> (8 * i));
+        }
+        if (sh == 3) {
+            dw[20] = last;
+        } else {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+                if ((uint32_t)i <= sh) dst[80 - (int)sh + i] = (uint8_t)(last >> (8 * i));
+        }
+    }
+}
+
 // ---- the wave-wide tail (plane_wide.h)
 // a record per handed-over board in the wave's staging area (stride: odd, so
 // 64 lanes writing one word each hit 64 banks): 27 plane words, board index
@@ -389,9 +462,11 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
 {
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
+    __shared__ __attribute__((aligned(16))) uint32_t outbox_lds[PLANE_THREADS / 64][PLANE_OUTBOX * PLANE_OB_WORDS];
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
+    uint32_t *outbox = outbox_lds[threadIdx.x >> 6];
+    uint32_t ob_count = 0;  // boards waiting in the outbox (wave-uniform)
     const uint8_t *stage_b = (const uint8_t *)stage;
-    sdk_v4u *stage4 = (sdk_v4u *)stage;  // the store path's slice records
     if ((threadIdx.x & 63) == 0) stage[PLANE_STAGE_DWORDS - 1] = 0u;  // the zero byte
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
@@ -480,55 +555,40 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
         if (__builtin_popcountll(~active) >= refill || active == 0) {
             const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
-            // ---- store finished boards.  Every solved lane first writes its
-            // board's value bit-slices (digit bit k of every cell, per band:
-            // 12 words) to the LDS staging area, all lanes at once; then the
-            // wave stores one board at a time, each lane reading the slices
-            // of its two cells' bands (same words for every lane: broadcast).
+            // ---- store finished boards, through the wave's LDS outbox: every
+            // solved lane appends its board's value bit-slices (12 words) and
+            // index; once 64 are waiting, each lane turns one of them into
+            // bytes and writes it as dwords (plane_flush_outbox).  No per-board
+            // serial loop: ~8 lane-parallel VALU per board instead of ~60
+            // wave instructions of per-board bookkeeping.
 #if SDK_PLANE_STAMPS
             const uint64_t st_s0 = __builtin_amdgcn_s_memtime();
 #endif
             uint64_t m = __builtin_amdgcn_ballot_w64(state == PL_SOLVED);
             solved += state == PL_SOLVED;
             if (m) {
+                const uint32_t ns = (uint32_t)__builtin_popcountll(m);
+                if (ob_count + ns > (uint32_t)PLANE_OUTBOX) {
+                    plane_flush_outbox(outbox, ob_count, lane, sols);
+                    ob_count = 0;
+                }
                 if (state == PL_SOLVED) {
-                    // value bit-slice k of band b, shifted left by k (bit pos + k
-                    // = bit k of the value at pos; bit 29 is a guard, so
-                    // nothing is lost), as one 16-byte record per (band, lane)
+                    sdk_v4u *rec = (sdk_v4u *)(outbox + PLANE_OB_WORDS * (ob_count + lanes_below(m)));
+                    uint32_t V[4][3];
 #pragma unroll
                     for (int b = 0; b < 3; ++b) {
-                        const uint32_t v0 = plane::or3(plane::or3(B.P[0][b], B.P[2][b], B.P[4][b]), B.P[6][b], B.P[8][b]);
-                        const uint32_t v1 = plane::or3(B.P[1][b], B.P[2][b], B.P[5][b] | B.P[6][b]);
-                        const uint32_t v2 = plane::or3(B.P[3][b], B.P[4][b], B.P[5][b] | B.P[6][b]);
-                        const uint32_t v3 = B.P[7][b] | B.P[8][b];
-                        const uint32_t v22 = v2 + v2, v33 = v3 + v3 + v3 + v3;
-                        stage4[b * 64 + lane] = (sdk_v4u){v0, v1 + v1, v22 + v22, v33 + v33};
+                        V[0][b] = plane::or3(plane::or3(B.P[0][b], B.P[2][b], B.P[4][b]), B.P[6][b], B.P[8][b]);
+                        V[1][b] = plane::or3(B.P[1][b], B.P[2][b], B.P[5][b] | B.P[6][b]);
+                        V[2][b] = plane::or3(B.P[3][b], B.P[4][b], B.P[5][b] | B.P[6][b]);
+                        V[3][b] = B.P[7][b] | B.P[8][b];
                     }
+                    rec[0] = (sdk_v4u){V[0][0], V[0][1], V[0][2], V[1][0]};
+                    rec[1] = (sdk_v4u){V[1][1], V[1][2], V[2][0], V[2][1]};
+                    rec[2] = (sdk_v4u){V[2][2], V[3][0], V[3][1], V[3][2]};
+                    rec[3] = (sdk_v4u){(uint32_t)p, (uint32_t)(p >> 32), 0u, 0u};
+                    status[p] = SDK_SOLVED;  // every solved lane its own, one store
                 }
-                const uint32_t pos = lane & 31, b0 = (uint32_t)lane >> 5;  // slot 0: band 0 / 1, slot 1: band 2
-                // software-pipelined: board i's records are read while the
-                // previous board's bytes go out
-                int i = __builtin_ctzll(m);
-                sdk_v4u t0 = stage4[b0 * 64 + i], t1 = stage4[2 * 64 + i];
-                for (;;) {
-                    const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
-                    m &= m - 1;
-                    const int in = m ? __builtin_ctzll(m) : i;
-                    const sdk_v4u n0 = stage4[b0 * 64 + in], n1 = stage4[2 * 64 + in];
-                    uint8_t *dst = sols + pi * 81;
-                    // value = bit k of (slice k << k) >> pos, k = 0..3
-                    const uint32_t v0 = plane::sel(7u, plane::sel(3u, plane::sel(1u, t0.x >> pos, t0.y >> pos), t0.z >> pos),
-                                                   t0.w >> pos) & 15u;
-                    const uint32_t v1 = plane::sel(7u, plane::sel(3u, plane::sel(1u, t1.x >> pos, t1.y >> pos), t1.z >> pos),
-                                                   t1.w >> pos) & 15u;
-                    if (c0 >= 0) dst[c0] = (uint8_t)v0;
-                    if (c1 >= 0) dst[c1] = (uint8_t)v1;
-                    if (!m) break;
-                    i = in;
-                    t0 = n0;
-                    t1 = n1;
-                }
-                if (state == PL_SOLVED) status[p] = SDK_SOLVED;  // every solved lane its own, one store
+                ob_count += ns;
             }
             // ---- unsolvable / cancelled: the input board back
             m = __builtin_amdgcn_ballot_w64(state >= PL_UNSOLVABLE);
@@ -740,6 +800,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             }
         }
     }
+    if (ob_count) plane_flush_outbox(outbox, ob_count, lane, sols);
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
 #endif
