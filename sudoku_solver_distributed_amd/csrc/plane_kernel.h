@@ -646,7 +646,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     queue_out = res_lo + c >= n;
                 }
                 base = (unsigned long long)res_lo;
-                const int kk = (int)(res_hi - res_lo < k ? res_hi - res_lo : k);
+                // (wave-uniform: readfirstlane keeps the deposit loop a scalar loop)
+                const int kk = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo < k ? res_hi - res_lo : k));
                 res_lo += kk;
                 drained = queue_out && res_lo == res_hi;
 #if SDK_PLANE_STAMPS
@@ -689,6 +690,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                         PLANE_DROP(2, 0, s2); PLANE_DROP(2, 1, s2 >> 32); PLANE_DROP(2, 2, u23);
                         PLANE_DROP(3, 0, s3); PLANE_DROP(3, 1, s3 >> 32); PLANE_DROP(3, 2, u23 >> 32);
 #undef PLANE_DROP
+                        // the next board's bytes are consumed here, after this
+                        // board's ballots: their LDS latency is hidden
+                        asm volatile("" ::"v"(n0), "v"(n1));
                         a0 = n0;
                         a1 = n1;
                     }
