@@ -35,7 +35,7 @@
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
 // $SDK_PLANE_TAIL, $SDK_PLANE_TAIL_MODE, $SDK_PLANE_CHUNK)
 #ifndef SDK_PLANE_REFILL
-#define SDK_PLANE_REFILL 12
+#define SDK_PLANE_REFILL 6
 #endif
 #ifndef SDK_PLANE_TAIL
 #define SDK_PLANE_TAIL 8
