@@ -104,21 +104,31 @@ def node_load(dev, requests: int = 2000, clients: int = 32):
 
 def e2e_rate(solver, boards, reps: int = 3):
     """PCIe-inclusive rate: pinned host boards in, host solutions and
-    statuses out (the serving path's view); `value` is device-resident."""
+    statuses out (the serving path's view; `value` is device-resident).
+    `serial`: copy in, solve, copy out back to back; `pipelined`:
+    BatchSolver.solve_host, chunks overlapping both copy directions with the
+    solve."""
     import torch
     host = boards.cpu().pin_memory()
     out_h = torch.empty_like(host).pin_memory()
     st_h = torch.empty(host.shape[0], dtype=torch.int32).pin_memory()
 
-    def run():
+    def serial():
         d = host.to(solver.device, non_blocking=True)
         sols, st = solver.solve(d)
         out_h.copy_(sols, non_blocking=True)
         st_h.copy_(st, non_blocking=True)
         return st_h
-    t, st = _time(run, reps)
-    return {"boards": host.shape[0], "ms": t * 1e3, "boards_per_s": host.shape[0] / t,
-            "all_solved": bool((st == 1).all())}
+
+    def pipelined():
+        return solver.solve_host(host, out=out_h, status=st_h)[1]
+    t, st = _time(serial, reps)
+    res = {"boards": host.shape[0], "ms": t * 1e3, "boards_per_s": host.shape[0] / t,
+           "all_solved": bool((st == 1).all())}
+    t, st = _time(pipelined, reps)
+    res["pipelined"] = {"ms": t * 1e3, "boards_per_s": host.shape[0] / t, "chunk": 1 << 18,
+                        "all_solved": bool((st == 1).all())}
+    return res
 
 
 def side_configs(solver, dev, world, rank, boards):

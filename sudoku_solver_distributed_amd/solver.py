@@ -129,6 +129,52 @@ class BatchSolver:
         _lib.check(rc, "sdk_solve_batch")
         return out, status
 
+    def solve_host(self, puzzles: torch.Tensor, order="gen", chunk: int = 1 << 18,
+                   out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None
+                   ) -> Tuple[torch.Tensor, torch.Tensor]:
+        """Host boards in, host solutions and statuses out (the serving
+        path), pipelined: chunk i+1 is copied in on one stream and chunk i-1
+        copied out on another while chunk i is solved, so both PCIe
+        directions overlap the kernel.  Give pinned host tensors (`out` /
+        `status` are allocated pinned when omitted); pageable input is copied
+        synchronously.  Same results as solve(); returns when all is back."""
+        p = as_boards(puzzles)
+        if p.device.type != "cpu":
+            raise ValueError("solve_host takes host boards; use solve() for device tensors")
+        n = p.shape[0]
+        if out is None:
+            out = torch.empty((n, 81), dtype=torch.uint8).pin_memory()
+        if status is None:
+            status = torch.empty(n, dtype=torch.int32).pin_memory()
+        if out.shape != (n, 81) or out.dtype != torch.uint8 or out.device.type != "cpu":
+            raise ValueError("out must be a host (n, 81) uint8 tensor")
+        if status.shape != (n,) or status.dtype != torch.int32 or status.device.type != "cpu":
+            raise ValueError("status must be a host (n,) int32 tensor")
+        if n == 0:
+            return out, status
+        d_in = torch.empty((n, 81), dtype=torch.uint8, device=self.device)
+        d_out = torch.empty_like(d_in)
+        d_st = torch.empty(n, dtype=torch.int32, device=self.device)
+        compute = torch.cuda.current_stream(self.device)
+        h2d = torch.cuda.Stream(self.device)
+        d2h = torch.cuda.Stream(self.device)
+        h2d.wait_stream(compute)  # the device buffers are compute-stream allocations
+        for lo in range(0, n, chunk):
+            hi = min(n, lo + chunk)
+            with torch.cuda.stream(h2d):
+                d_in[lo:hi].copy_(p[lo:hi], non_blocking=True)
+            compute.wait_stream(h2d)
+            self.solve(d_in[lo:hi], out=d_out[lo:hi], status=d_st[lo:hi], order=order, stream=compute)
+            d2h.wait_stream(compute)
+            with torch.cuda.stream(d2h):
+                out[lo:hi].copy_(d_out[lo:hi], non_blocking=True)
+                status[lo:hi].copy_(d_st[lo:hi], non_blocking=True)
+        for t in (d_in, d_out, d_st):
+            t.record_stream(h2d)
+            t.record_stream(d2h)
+        d2h.synchronize()
+        return out, status
+
     def check(self, grids, mode: int = 0, stream=None) -> torch.Tensor:
         """mode 0: Sudoku.check (sudoku.py:119-140); mode 1: node.py:82-116."""
         g = self._dev(as_boards(grids, max_value=255))

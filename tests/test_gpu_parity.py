@@ -469,3 +469,16 @@ def test_plane_tail_paths(solver, tail, mode):
     finally:
         lib.sdk_set_plane_tuning(-1, -1, -1, -1)
         lib.sdk_set_solve_kernel(prev)
+
+
+def test_solve_host_pipelined(solver):
+    """BatchSolver.solve_host (chunks overlapping H2D / solve / D2H on three
+    streams) returns exactly what solve() returns, for ragged chunking."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    boards = torch.cat([hard17_batch(20000, seed=41), torch.zeros((3, 81), dtype=torch.uint8)])
+    want, wst = solver.solve(boards.to(solver.device))
+    got, gst = solver.solve_host(boards.pin_memory(), chunk=8192)
+    assert got.device.type == "cpu" and gst.device.type == "cpu"
+    assert torch.equal(got, want.cpu()) and torch.equal(gst, wst.cpu())
+    got, gst = solver.solve_host(boards[:5])  # pageable, one chunk
+    assert torch.equal(got, want[:5].cpu())
