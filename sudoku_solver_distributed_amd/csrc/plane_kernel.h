@@ -12,8 +12,10 @@
 // guesses push the 27 words + the branch entry to the lane's stack lines in
 // the workspace (PlaneStack).  Finished lanes wait until at least
 // SDK_PLANE_REFILL lanes of the wave are free, then stores and refills run
-// once for all of them (the 81-byte I/O is wave-cooperative).  Boards come
-// from a static first hand-out and then chunked claims on one queue head.
+// once for all of them: solved boards go to the wave's LDS outbox (written
+// out 64 at a time, a board per lane, as dwords), new boards come in as one
+// staged span (wave-cooperative ballots).  Boards come from a static first
+// hand-out and then chunked claims on one queue head.
 //
 // Once the queue is empty, a wave down to SDK_PLANE_TAIL boards hands them to
 // the wave-wide solver (plane_wide.h): each board in turn is spread over the
