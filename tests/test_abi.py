@@ -71,3 +71,22 @@ def test_no_wide_store_data_hazard():
     assert not H.scan(["buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen", "s_nop 1",
                        "v_mov_b32 v1, v2"])
     assert H.main() == 0
+
+
+def test_plane_tuning_arguments():
+    """sdk_set_plane_tuning (host-only code, no GPU needed): out-of-range
+    values are refused and change nothing, negatives keep a knob, all four
+    negative restore the defaults."""
+    from sudoku_solver_distributed_amd import _lib, build
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.sdk_set_plane_tuning
+    f.restype = ctypes.c_int
+    f.argtypes = [ctypes.c_int] * 4
+    assert f(65, -1, -1, -1) == -1      # refill > 64
+    assert f(0, -1, -1, -1) == -1       # refill 0: a wave would never refill
+    assert f(-1, 41, -1, -1) == -1      # tail > 40 (LDS records)
+    assert f(-1, -1, 2, -1) == -1       # tail mode 0 / 1 only
+    assert f(8, 40, 0, 32) == 0
+    assert f(-1, 0, -1, -1) == 0        # tail off
+    assert f(-1, -1, -1, -1) == 0       # defaults back
