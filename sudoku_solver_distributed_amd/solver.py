@@ -82,6 +82,7 @@ class BatchSolver:
         self._last_stream = None
         # held by callers that need solve + stats as one step (node.py's backend)
         self.op_lock = threading.RLock()
+        self._copy_streams = None  # solve_host's copy-in / copy-out streams
         with torch.cuda.device(self.device):
             self.workspace = torch.zeros(int(self.lib.sdk_workspace_bytes()), dtype=torch.uint8,
                                          device=self.device)
@@ -156,8 +157,11 @@ class BatchSolver:
         d_out = torch.empty_like(d_in)
         d_st = torch.empty(n, dtype=torch.int32, device=self.device)
         compute = torch.cuda.current_stream(self.device)
-        h2d = torch.cuda.Stream(self.device)
-        d2h = torch.cuda.Stream(self.device)
+        if self._copy_streams is None:
+            # created once: each new stream takes a hardware queue slot, and
+            # past the process's few queues streams share them (and serialise)
+            self._copy_streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
+        h2d, d2h = self._copy_streams
         h2d.wait_stream(compute)  # the device buffers are compute-stream allocations
         for lo in range(0, n, chunk):
             hi = min(n, lo + chunk)
