@@ -44,7 +44,8 @@ extern "C" {
  * the library re-arms the per-call words itself on `stream`.
  * A workspace is SINGLE-STREAM: every call that passes the same workspace
  * must be issued on the same stream (or ordered by the caller), because each
- * sdk_solve_batch re-arms the workspace's queue head before its kernels.
+ * sdk_solve_batch re-arms the workspace's queue head before its kernels when
+ * they use it (not for a small unordered batch the static hand-out covers).
  * Enqueueing is thread-safe (the library serialises its launch sequences). */
 size_t sdk_workspace_bytes(void);
 

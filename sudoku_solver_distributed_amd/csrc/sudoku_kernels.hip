@@ -509,10 +509,13 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
     int variant = solve_variant();
     if (variant == SDK_KERNEL_AUTO) variant = n >= SDK_PLANE_MIN_BATCH ? SDK_KERNEL_PLANE : SDK_KERNEL_PACKED;
     std::lock_guard<std::mutex> lk(g_launch_mu);
-    hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     hipError_t e;
     if (variant == SDK_KERNEL_PACKED) {
         const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_kernel, g_bpc_packed) * WAVES_PER_BLOCK;
+        // A batch the static hand-out covers (one board per wave) never uses
+        // the queue head's value, and an unordered one not the best word:
+        // no re-arm launch then (a single board's latency: -1 launch)
+        if (ordered || n > max_waves) hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
         const int64_t waves = n < max_waves ? n : max_waves;
         int64_t chunk = n / (waves * 16);
         if (chunk < 1) chunk = 1;
@@ -521,6 +524,7 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
         hipLaunchKernelGGL(solvep_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
                            d_status, n, ws, chunk, ordered, order);
     } else {
+        hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
         // lanes: one per board up to a full grid; the stacks sit in the workspace
         const int64_t max_threads = plane_max_threads();
         const int64_t threads = n < max_threads ? n : max_threads;
