@@ -307,17 +307,20 @@ PS_FN void set_cell(Board &B, int band, int pos, uint32_t dbit)
 // E[b]: empty cells.  Returns the given cells (non-empty).
 PS_FN void planes_from_slices(Board &B, const uint32_t (&V)[4][3], uint32_t (&given)[3])
 {
+    // value v = (v1 v0) + 4 (v3 v2): one-hot over the low pair and over the
+    // high pair, then each digit's plane is one AND of the two (plus the
+    // empty cells): 18 operations per band instead of ~43
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
-        const uint32_t v0 = V[0][b], v1 = V[1][b], v2 = V[2][b], v3 = V[3][b];
-        const uint32_t n0 = ROWS & ~v0, n1 = ROWS & ~v1, n2 = ROWS & ~v2, n3 = ROWS & ~v3;
-        const uint32_t e = n0 & n1 & n2 & n3;
-        given[b] = ROWS & ~e;
+        const uint32_t v0 = V[0][b], v1 = V[1][b], v2 = V[2][b], v3 = V[3][b];  // cell bits only
+        const uint32_t lo[4] = {andn2(ROWS, v0, v1), andn(v0, v1), andn(v1, v0), v0 & v1};
+        const uint32_t hi[3] = {andn2(ROWS, v2, v3), andn(v2, v3), andn(v3, v2)};
+        const uint32_t e = lo[0] & hi[0];
+        given[b] = andn(ROWS, e);
 #pragma unroll
         for (int d = 0; d < 9; ++d) {
             const int v = d + 1;
-            const uint32_t eq = ((v & 1) ? v0 : n0) & ((v & 2) ? v1 : n1) & ((v & 4) ? v2 : n2) & ((v & 8) ? v3 : n3);
-            B.P[d][b] = eq | e;
+            B.P[d][b] = or_and(e, lo[v & 3], hi[v >> 2]);
         }
         B.Det[b] = 0;
     }
