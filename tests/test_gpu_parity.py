@@ -482,3 +482,32 @@ def test_solve_host_pipelined(solver):
     assert torch.equal(got, want.cpu()) and torch.equal(gst, wst.cpu())
     got, gst = solver.solve_host(boards[:5])  # pageable, one chunk
     assert torch.equal(got, want[:5].cpu())
+
+
+@pytest.mark.parametrize("refill,chunk", [(1, 0), (64, 255)])
+def test_plane_refill_extremes(solver, refill, chunk):
+    """The plane kernel's I/O at extreme knobs (sdk_set_plane_tuning):
+    refill at every free lane with one queue claim per refill, and refill only
+    when the whole wave is idle with the largest claims -- on a batch larger
+    than the grid, so static hand-out, claims, outbox flushes and the tail
+    all run.  Every board solved, passing Sudoku.check, givens kept, and a
+    sample equal to its unique completion."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    lib = solver.lib
+    prev = lib.sdk_set_solve_kernel(_lib.SDK_KERNELS["plane"])
+    assert lib.sdk_set_plane_tuning(refill, -1, -1, chunk) == 0
+    try:
+        boards = hard17_batch(300_000, seed=51)
+        d = boards.to(solver.device)
+        sols, st = solver.solve(d)
+        assert bool((st == 1).all())
+        assert bool((solver.check(sols, 0) == 1).all())
+        given = d != 0
+        assert bool((sols[given] == d[given]).all())
+        idx = np.random.default_rng(51).choice(boards.shape[0], 2000, replace=False)
+        want, cnt = O.solve_unique_batch(boards[idx].numpy())
+        assert (cnt == 1).all() and np.array_equal(sols[idx].cpu().numpy(), want)
+    finally:
+        lib.sdk_set_plane_tuning(-1, -1, -1, -1)
+        lib.sdk_set_solve_kernel(prev)
