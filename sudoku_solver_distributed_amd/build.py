@@ -15,8 +15,31 @@ ROOT = os.path.dirname(_HERE)
 # (iterative-ilp measured +1.4 % over LLVM's default on one MI355X, same
 # registers; "default" = LLVM's own, for A/B builds)
 _SCHED = os.environ.get("SDK_PLANE_SCHED", "iterative-ilp")
-SRCS = (("sudoku_kernels.hip", []),
-        ("plane_kernels.hip", [] if _SCHED == "default" else ["-mllvm", f"-amdgpu-sched-strategy={_SCHED}"]))
+
+
+def sources(sched: str = _SCHED):
+    """Translation units and their flags for one plane-unit scheduler."""
+    return (("sudoku_kernels.hip", []),
+            ("plane_kernels.hip", [] if sched == "default" else ["-mllvm", f"-amdgpu-sched-strategy={sched}"]))
+
+
+SRCS = sources()
+# Every build this module is used for (product, diagnostic and A/B tuning
+# builds): name -> (-D set, plane-unit scheduler).  scripts/store_hazard_check.py
+# scans each of them for the wide-store data hazard; build() scans any other
+# -D set before linking it.
+VARIANTS = {
+    "default": ((), _SCHED),
+    "stamps": (("SDK_PLANE_STAMPS=1",), _SCHED),
+    "waves5": (("SDK_PLANE_WAVES_PER_EU=5",), _SCHED),
+    "waves6": (("SDK_PLANE_WAVES_PER_EU=6",), _SCHED),
+    "nopinacc": (("SDK_PLANE_PIN_ACC=0",), _SCHED),
+    "tail_restart": (("SDK_PLANE_TAIL_MODE=0",), _SCHED),
+    "sched-default": ((), "default"),
+    "sched-minreg": ((), "iterative-minreg"),
+    "sched-maxocc": ((), "iterative-maxocc"),
+    "sched-max-ilp": ((), "max-ilp"),
+}
 OUT = os.path.join(_HERE, "libsudoku_hip.so")
 ARCH = os.environ.get("SDK_OFFLOAD_ARCH", "gfx950")
 
@@ -37,6 +60,12 @@ def build(force: bool = False, verbose: bool = False, defines=(), out: str = OUT
     if (not force and os.path.exists(out)
             and all(os.path.getmtime(out) >= os.path.getmtime(d) for d in deps)):
         return out
+    if tuple(defines) and tuple(defines) not in {v[0] for v in VARIANTS.values()}:
+        # an A/B build nobody has scanned yet: the wide-store hazard check first
+        sys.path.insert(0, os.path.join(ROOT, "scripts"))
+        import store_hazard_check
+        if store_hazard_check.check_build(SRCS, defines, "+".join(defines)):
+            raise RuntimeError(f"wide-store data hazard in the build with {defines} (scripts/store_hazard_check.py)")
     objs = []
     for name, extra in SRCS:
         obj = out + "." + name + ".o"

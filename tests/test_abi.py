@@ -66,11 +66,18 @@ def test_no_wide_store_data_hazard():
     import sys
     sys.path.insert(0, os.path.join(ROOT, "scripts"))
     import store_hazard_check as H
-    assert H.scan(["buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen",
-                   "v_bitop3_b32 v1, v28, 1, v56 bitop3:0x80"])  # the pattern that corrupted the stack
-    assert not H.scan(["buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen", "s_nop 1",
-                       "v_mov_b32 v1, v2"])
-    assert H.main() == 0
+    st = "buffer_store_dwordx4 v[0:3], v64, s[0:3], s4 offen"
+    assert H.scan([st, "v_bitop3_b32 v1, v28, 1, v56 bitop3:0x80"])  # the pattern that corrupted the stack
+    # the window is two wait states: a write at distance 2, or behind one
+    # s_nop 0, is still a hazard; s_nop 1 (two states) or two instructions clear it
+    assert H.scan([st, "s_movk_i32 s0, 0x60", ";;#ASMSTART", "v_mov_b32 v3, v9"])
+    assert H.scan([st, "s_nop 0", "v_mov_b32 v2, v9"])
+    assert H.scan(["global_store_dwordx3 v5, v[10:12], s[2:3]", "v_add_u32 v12, v1, v2"])
+    assert not H.scan([st, "s_nop 1", "v_mov_b32 v1, v2"])
+    assert not H.scan([st, "s_mov_b32 s0, 1", "s_mov_b32 s1, 1", "v_mov_b32 v1, v2"])
+    assert not H.scan([st, "v_mov_b32 v64, v2"])  # the address is read at issue
+    assert not H.scan(["buffer_store_dwordx2 v[0:1], v64, s[0:3], s4 offen", "v_mov_b32 v1, v2"])  # 64-bit
+    assert H.main() == 0  # every build variant (build.VARIANTS)
 
 
 def test_plane_tuning_arguments():
