@@ -76,7 +76,8 @@ int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
                               int32_t *d_num, int64_t n, void *stream);
 
 /* The reference's HTTP /solve algorithm, node.py:534-557
- * P2PNode.peer_sudoku_solve on a fresh single node (handicap 0, no peers):
+ * P2PNode.peer_sudoku_solve, one FRESH single node per board (handicap 0, no
+ * peers; sdk_peer_solve_seq below carries one node's state across requests):
  * a greedy row-major cell loop with node.py's repair step (node.py:419-532),
  * not a search.  d_out[i] = the board it leaves (valid or not), d_status[i] =
  * SDK_SOLVED (its final check passed), SDK_UNSOLVABLE (returned, check
@@ -86,6 +87,22 @@ int sdk_first_candidate_batch(const uint8_t *d_grids, const int32_t *d_cells,
  * SudokuSolver.check: every is_valid_move plus the final check). */
 int sdk_peer_solve_batch(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_status, int32_t *d_validations,
                          int64_t n, void *stream);
+
+/* The same /solve loop on ONE P2PNode serving n requests in order
+ * (node.py:534-557, requests 0..n-1 as the reference's single-threaded
+ * HTTPServer would take them).  The node keeps partial_solution and
+ * tried_numbers_by_position (node.py:149, 167) across requests, and a later
+ * request's repair step (node.py:501-506) reads what earlier ones left, so
+ * request i starts from the state request i-1 left.  d_node_state: one
+ * SDK_PEER_STATE_BYTES record in device memory, in/out (all zero = a new
+ * node).  Outputs per request as sdk_peer_solve_batch; d_validations[i] is
+ * the counter's increase during request i.  A request with a byte > 9 gets
+ * SDK_INVALID and leaves the node as it was.  After SDK_NO_RETURN the
+ * reference node spins forever and serves nothing more; this call goes on
+ * from the state the loop spun in. */
+#define SDK_PEER_STATE_BYTES 1600
+int sdk_peer_solve_seq(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_status, int32_t *d_validations,
+                       int64_t n, void *d_node_state, void *stream);
 
 /* One level of the reference walk's search tree, for splitting a single hard
  * board over waves / GPUs (node.py's per-cell peer task split, node.py:419-449,
@@ -114,6 +131,12 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
  * its stack, the last few boards of a wave once the queue is empty).
  * reset != 0 zeroes them afterwards. */
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
+
+/* The same six counters as sdk_read_stats, copied to DEVICE memory d_out[6]
+ * asynchronously on `stream` (stream-ordered with the solves on that
+ * workspace: two snapshots around a solve give that solve's own counts
+ * without a host synchronisation). */
+int sdk_snapshot_stats(const void *d_workspace, int64_t *d_out, void *stream);
 
 /* Solve-kernel selection (library extension, no reference counterpart):
  * SDK_KERNEL_AUTO (default) SDK_KERNEL_PLANE for batches of 8192 boards or

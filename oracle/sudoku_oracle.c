@@ -398,8 +398,13 @@ int64_t oracle_solve_batch_timed(const uint8_t *in, uint8_t *out, int32_t *statu
 }
 
 /* ------------------------------------------------------------------------
- * node.py:534-557 P2PNode.peer_sudoku_solve on a FRESH single node (no
- * peers, handicap 0): the reference's HTTP /solve path.
+ * node.py:534-557 P2PNode.peer_sudoku_solve on a single node (no peers,
+ * handicap 0): the reference's HTTP /solve path.  The node's
+ * partial_solution and tried_numbers_by_position (node.py:149, 167) live in
+ * the P2PNode and survive from one request to the next (peer_sudoku_solve
+ * resets initial_sudoku, sudoku and the task queue only, node.py:539-552):
+ * oracle_peer_solve_node takes them in and leaves them updated;
+ * oracle_peer_solve is a fresh node (both empty).
  *   fill_task_queue (node.py:419-425): the empty cells, row-major;
  *   solve_sudoku (node.py:427-475): pop a cell, take the first digit that
  *     is_valid_move accepts (solve_sudoku_destributed, node.py:76-80; with
@@ -421,15 +426,15 @@ static int peer_valid_move(const uint8_t *g, int row, int col, int num)
     return oracle_is_valid_move(g, row, col, num);
 }
 
-int oracle_peer_solve(uint8_t *sudoku, int32_t *validations)
+/* partial[cell] = digit placed by the loop, 0 = absent (partial_solution);
+ * tried[(row,col)][c*9 + v-1]: (row, c, v) in tried_numbers_by_position[(row,
+ * col)] (the row is implied: node.py:523 adds (r, c, value) with r == row) */
+int oracle_peer_solve_node(uint8_t *sudoku, int32_t *validations, uint8_t partial[81], uint8_t tried[81][81])
 {
-    uint8_t initial[81], partial[81]; /* partial[cell] = digit, 0 = absent */
-    uint8_t tried[81][81];            /* tried[(row,col)][c*9 + v-1]: (row, c, v) tried; row is implied */
+    uint8_t initial[81];
     int queue[1024], qh = 512, qt = 512; /* deque: popleft at qh, append at qt, appendleft at --qh */
     int flag = 1;
     memcpy(initial, sudoku, 81);
-    memset(partial, 0, sizeof partial);
-    memset(tried, 0, sizeof tried);
     g_val = 0;
     for (int i = 0; i < 81; i++)
         if (sudoku[i] == 0) queue[qt++] = i;
@@ -496,4 +501,12 @@ int oracle_peer_solve(uint8_t *sudoku, int32_t *validations)
     g_val++;                                 /* node.py:466 self.solver.check(self.sudoku) */
     *validations = g_val;
     return oracle_check_sums(sudoku) ? 1 : 0;
+}
+
+int oracle_peer_solve(uint8_t *sudoku, int32_t *validations)
+{
+    uint8_t partial[81], tried[81][81];
+    memset(partial, 0, sizeof partial);
+    memset(tried, 0, sizeof tried);
+    return oracle_peer_solve_node(sudoku, validations, partial, tried);
 }

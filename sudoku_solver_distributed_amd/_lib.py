@@ -18,6 +18,7 @@ SDK_SOLVED = 1
 SDK_INVALID = -1
 SDK_CANCELLED = -2
 SDK_NO_RETURN = -4   # sdk_peer_solve_batch: node.py's /solve loop never returns
+SDK_PEER_STATE_BYTES = 1600  # sdk_peer_solve_seq: one node's partial_solution + tried sets
 SDK_ORDER_GEN = 0    # gen.py:6-28's walk (last row with an empty cell first)
 SDK_ORDER_NODE = 1   # node.py:62-74's walk (row-major)
 ORDERS = {"gen": SDK_ORDER_GEN, "node": SDK_ORDER_NODE}
@@ -29,8 +30,10 @@ EXPORTS = (
     "sdk_check_batch",
     "sdk_first_candidate_batch",
     "sdk_peer_solve_batch",
+    "sdk_peer_solve_seq",
     "sdk_expand_frontier",
     "sdk_read_stats",
+    "sdk_snapshot_stats",
     "sdk_last_error",
     "sdk_version",
     "sdk_device_cu_count",
@@ -69,10 +72,14 @@ def load() -> ctypes.CDLL:
     L.sdk_first_candidate_batch.argtypes = [vp, vp, vp, i64, vp]
     L.sdk_peer_solve_batch.restype = i32
     L.sdk_peer_solve_batch.argtypes = [vp, vp, vp, vp, i64, vp]
+    L.sdk_peer_solve_seq.restype = i32
+    L.sdk_peer_solve_seq.argtypes = [vp, vp, vp, vp, i64, vp, vp]
     L.sdk_expand_frontier.restype = i32
     L.sdk_expand_frontier.argtypes = [vp, i64, vp, vp, vp, i64, i32, vp]
     L.sdk_read_stats.restype = i32
     L.sdk_read_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i32, vp]
+    L.sdk_snapshot_stats.restype = i32
+    L.sdk_snapshot_stats.argtypes = [vp, vp, vp]
     L.sdk_last_error.restype = ctypes.c_char_p
     L.sdk_last_error.argtypes = []
     L.sdk_version.restype = ctypes.c_char_p

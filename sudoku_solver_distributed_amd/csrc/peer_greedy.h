@@ -13,6 +13,13 @@
 // The answer is whatever board is left, valid or not; `validations` counts
 // node.py's SudokuSolver.check calls (every is_valid_move and the final
 // check), as node.py:87 does.
+//
+// A P2PNode keeps partial_solution and tried_numbers_by_position (node.py:
+// 149, 167) from one /solve request to the next: peer_sudoku_solve resets
+// initial_sudoku, sudoku and the task queue only (node.py:539-552), so the
+// repair step of a later request can take over a digit "placed" in an
+// earlier board.  That part of the state is NodeState; run() starts from it
+// (a fresh node: all zero) and leaves it as node.py would.
 #ifndef SDK_PEER_GREEDY_H
 #define SDK_PEER_GREEDY_H
 
@@ -56,13 +63,30 @@ PG_FN bool valid_move(const uint8_t *g, int row, int col, int num, int &checks)
     return true;
 }
 
+// the node's state that outlives a request (the C ABI's SDK_PEER_STATE_BYTES
+// record, byte for byte)
+struct NodeState {
+    uint8_t placed[81];      // partial_solution: digit the loop put in the cell, 0 = none
+    uint8_t pad0[15];
+    uint16_t tried[81][9];   // tried_numbers_by_position[(r,c)]: bit v-1 of [c'] = (r, c', v) tried
+    uint8_t pad1[46];
+};
+static_assert(sizeof(NodeState) == 1600, "SDK_PEER_STATE_BYTES");
+
 struct State {
     uint8_t sudoku[81], initial[81];
-    uint8_t placed[81];      // partial_solution: digit this loop put in the cell, 0 = none
-    uint16_t tried[81][9];   // tried_numbers_by_position[(r,c)]: bit v-1 of [c'] = (r, c', v) tried
+    NodeState node;
     uint8_t ring[128];       // task_queue: a deque of cell indices (never longer than 81)
     uint32_t head, tail;     // ring[head % 128] is the left end, ring[(tail - 1) % 128] the right
 };
+
+PG_FN void clear_node(NodeState &n)
+{
+    for (int k = 0; k < 81; ++k) {
+        n.placed[k] = 0;
+        for (int c = 0; c < 9; ++c) n.tried[k][c] = 0;
+    }
+}
 
 PG_FN void push_left(State &s, int cell) { s.ring[(--s.head) & 127u] = (uint8_t)cell; }
 PG_FN int pop_left(State &s) { return s.ring[(s.head++) & 127u]; }
@@ -76,23 +100,23 @@ PG_FN bool repair(State &s, int cell, int &checks)
     int cand[9], nc = 0;
     for (int c = 0; c < 9; ++c) {
         const int rc = 9 * row + c;
-        if (c == col || !s.placed[rc]) continue;
-        const int v = s.placed[rc];
+        if (c == col || !s.node.placed[rc]) continue;
+        const int v = s.node.placed[rc];
         temp[rc] = 0;  // the zeros accumulate along the row, as in node.py:503
-        if (valid_move(temp, row, col, v, checks) && v != s.initial[rc] && !((s.tried[cell][c] >> (v - 1)) & 1u))
+        if (valid_move(temp, row, col, v, checks) && v != s.initial[rc] && !((s.node.tried[cell][c] >> (v - 1)) & 1u))
             cand[nc++] = c;
     }
     const int br = 3 * (row / 3), bc = 3 * (col / 3);
     for (int k = 0; k < nc; ++k) {
-        const int c = cand[k], rc = 9 * row + c, v = s.placed[rc];
+        const int c = cand[k], rc = 9 * row + c, v = s.node.placed[rc];
         bool safe = true;
         for (int t = 0; t < 9 && safe; ++t)
             safe = temp[9 * row + t] != v && temp[9 * t + col] != v && temp[9 * (br + t / 3) + bc + t % 3] != v;
         if (safe) {
             s.sudoku[cell] = (uint8_t)v;
-            s.placed[cell] = (uint8_t)v;
-            s.placed[rc] = 0;
-            s.tried[cell][c] |= (uint16_t)(1u << (v - 1));
+            s.node.placed[cell] = (uint8_t)v;
+            s.node.placed[rc] = 0;
+            s.node.tried[cell][c] |= (uint16_t)(1u << (v - 1));
             s.sudoku[rc] = 0;
             push_left(s, rc);
             return true;
@@ -102,15 +126,14 @@ PG_FN bool repair(State &s, int cell, int &checks)
     return false;
 }
 
-// The whole loop on s.sudoku (filled in by the caller); returns PG_*.
+// The whole loop on s.sudoku (filled in by the caller) from the node state
+// in s.node (clear_node() first for a fresh node); returns PG_*.
 PG_FN int run(State &s, int &checks)
 {
     checks = 0;
     s.head = s.tail = 64;
     for (int k = 0; k < 81; ++k) {
         s.initial[k] = s.sudoku[k];
-        s.placed[k] = 0;
-        for (int c = 0; c < 9; ++c) s.tried[k][c] = 0;
         if (!s.sudoku[k]) s.ring[(s.tail++) & 127u] = (uint8_t)k;
     }
     bool flag = true;
@@ -123,7 +146,7 @@ PG_FN int run(State &s, int &checks)
             if (num) {
                 if (valid_move(s.sudoku, row, col, num, checks)) {  // node.py:480 (same board: accepted)
                     s.sudoku[cell] = (uint8_t)num;
-                    s.placed[cell] = (uint8_t)num;
+                    s.node.placed[cell] = (uint8_t)num;
                 } else {
                     push_left(s, cell);
                 }

@@ -234,10 +234,40 @@ __global__ __launch_bounds__(64) void peer_solve_kernel(const uint8_t *__restric
         return;
     }
     int checks = 0;
+    peer::clear_node(s.node);  // a fresh node per board
     const int r = peer::run(s, checks);
     for (int k = 0; k < 81; ++k) dst[k] = s.sudoku[k];
     status[i] = r == peer::PG_CHECKED ? SDK_SOLVED : r == peer::PG_CHECK_FAILED ? SDK_UNSOLVABLE : SDK_NO_RETURN;
     validations[i] = checks;
+}
+
+// ONE node serving n requests in order (sdk_peer_solve_seq): a single lane
+// walks them, the node's partial_solution / tried sets carried from each
+// request to the next through `node` (device memory, in and out)
+__global__ __launch_bounds__(64) void peer_seq_kernel(const uint8_t *__restrict__ boards, uint8_t *__restrict__ out,
+                                                      int32_t *__restrict__ status,
+                                                      int32_t *__restrict__ validations, int64_t n,
+                                                      peer::NodeState *__restrict__ node)
+{
+    if (threadIdx.x != 0) return;
+    peer::State s;
+    s.node = *node;
+    for (int64_t i = 0; i < n; ++i) {
+        const uint8_t *src = boards + i * 81;
+        uint8_t *dst = out + i * 81;
+        bool bad = false;
+        for (int k = 0; k < 81; ++k) {
+            s.sudoku[k] = src[k];
+            bad |= s.sudoku[k] > 9;
+        }
+        int checks = 0, r = -1;
+        if (!bad) r = peer::run(s, checks);  // a rejected request leaves the node as it was
+        for (int k = 0; k < 81; ++k) dst[k] = s.sudoku[k];
+        status[i] = bad ? SDK_INVALID
+                        : r == peer::PG_CHECKED ? SDK_SOLVED : r == peer::PG_CHECK_FAILED ? SDK_UNSOLVABLE : SDK_NO_RETURN;
+        validations[i] = checks;
+    }
+    *node = s.node;
 }
 
 // ------------------------------------------------------ frontier expansion
@@ -610,6 +640,21 @@ int sdk_peer_solve_batch(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_sta
     return e == hipSuccess ? 0 : set_err("sdk_peer_solve_batch: launch", e);
 }
 
+int sdk_peer_solve_seq(const uint8_t *d_boards, uint8_t *d_out, int32_t *d_status, int32_t *d_validations, int64_t n,
+                       void *d_node_state, void *stream)
+{
+    static_assert(sizeof(peer::NodeState) == SDK_PEER_STATE_BYTES, "node state record");
+    if (n < 0 || !d_node_state || (n > 0 && (!d_boards || !d_out || !d_status || !d_validations))) {
+        snprintf(g_err, sizeof g_err, "sdk_peer_solve_seq: bad arguments");
+        return -2;
+    }
+    if (n == 0) return 0;
+    hipLaunchKernelGGL(peer_seq_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, d_boards, d_out, d_status,
+                       d_validations, n, (peer::NodeState *)d_node_state);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_peer_solve_seq: launch", e);
+}
+
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
 {
     if (!d_workspace || !out) {
@@ -633,6 +678,25 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
         if (e != hipSuccess) return set_err("sdk_read_stats: reset", e);
     }
     return 0;
+}
+
+__global__ void snapshot_stats_kernel(const unsigned long long *__restrict__ ws, int64_t *__restrict__ out)
+{
+    const int i = threadIdx.x;
+    const int word[6] = {WS_FINISHED, WS_SOLVED, WS_GUESSES, WS_SWEEPS, WS_BEST, WS_DEFERRED};
+    if (i < 6) out[i] = (int64_t)ws[word[i]];
+}
+
+int sdk_snapshot_stats(const void *d_workspace, int64_t *d_out, void *stream)
+{
+    if (!d_workspace || !d_out) {
+        snprintf(g_err, sizeof g_err, "sdk_snapshot_stats: bad arguments");
+        return -2;
+    }
+    hipLaunchKernelGGL(snapshot_stats_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                       (const unsigned long long *)d_workspace, d_out);
+    hipError_t e = hipGetLastError();
+    return e == hipSuccess ? 0 : set_err("sdk_snapshot_stats: launch", e);
 }
 
 }  // extern "C"

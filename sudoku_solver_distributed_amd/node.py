@@ -10,9 +10,14 @@ What changed against node.py (and why):
 * ``SudokuSolver`` (node.py:21-131) keeps its methods and counters; the
   walk (`solve_sudoku`, `solve_sudoku_recursive`, node.py:31-40/62-74), the
   check (node.py:82-116) and the per-cell task (`solve_sudoku_destributed`,
-  node.py:76-80) are HIP kernels.  `validations` counts what the reference
-  counts (one per check() call) plus, for a GPU solve, the kernel's
-  propagation passes (each one validates every empty cell once).
+  node.py:76-80) are HIP kernels.  `validations`: the
+  reference adds one per SudokuSolver.check call (node.py:87), and its walk
+  calls check once per candidate test (is_valid_move, node.py:44, 68) --
+  ~1e7-1e8 per hard board, a number only the literal walk itself can count.
+  Here a check() / is_valid_move / cell task still adds one each; a walk
+  solve on the GPU adds the kernel's propagation passes over the board (one
+  pass tests every empty cell against its row, column and box once), and a
+  solve in "reference" mode adds exactly the reference's count.
 * Every board a peer is asked to solve -- HTTP `/solve` (node.py:672-690),
   a UDP `solve` message, `SudokuSolver.solve_sudoku` -- goes through one
   ``BoardBatcher`` per peer: concurrent requests are coalesced into one GPU
@@ -27,12 +32,16 @@ What changed against node.py (and why):
   or more hands new boards to its peers (round robin, UDP `solve` with a
   `task` id, answered by a `solution` message) and solves locally if a peer
   does not answer in time.  The answer is node.py's recursive walk
-  (node.py:62-74), bit-identical; the reference's HTTP path answers with its
-  greedy task loop instead, which differs on some boards (INTEGRATION.md §3,
-  tests/golden/golden_peer.json).
+  (node.py:62-74), bit-identical.  The reference's HTTP path answers with its
+  greedy task loop instead, which differs on some boards; solve_mode
+  "reference" reproduces that loop, including the state a reference node
+  carries from one request to the next (INTEGRATION.md §3,
+  tests/golden/golden_peer.json, golden_peer_seq.json).
 * The UDP `solve` / `solution` messages (node.py:384-406) are kept: with
   `row`/`col` they are the reference's cell task; without them a peer hands
-  a whole board (`sudoku`) or a batch (`sudokus`, 81-character strings).
+  a whole board (`sudoku`) or a batch (`sudokus`, 81-character strings, at
+  most MAX_UDP_BOARDS per datagram).  Every `solve` is answered, with an
+  `error` field if it could not be served.
 * Membership and statistics messages (`connect`, `connected`, `all_peers`,
   `disconnect`, `stats`; node.py:193-382) keep their JSON shape.
 * The HTTP server binds a configurable host (node.py:708 hard-codes a LAN IP)
@@ -48,68 +57,115 @@ import socket
 import threading
 import time
 from collections import deque
-from concurrent.futures import Future
+from concurrent.futures import Future, ThreadPoolExecutor
 from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import List, Optional
 
 import torch
 
-from .solver import SDK_NO_RETURN, SDK_SOLVED, as_boards, get_solver
+from .solver import SDK_NO_RETURN, SDK_SOLVED, BatchSolver, as_boards, get_solver
 
 logger = logging.getLogger(__name__)
 
+# boards per UDP `sudokus` message: 81 characters + JSON punctuation each, so
+# the request (and the reply, which adds a status per board) stays well inside
+# one datagram (65 507 bytes of payload)
+MAX_UDP_BOARDS = 256
+BATCH_ORDERS = ("gen", "node")
+
+
+def is_grid9(board) -> bool:
+    """Exactly the reference's board type: 9 lists of 9 integers."""
+    return (isinstance(board, list) and len(board) == 9
+            and all(isinstance(r, list) and len(r) == 9 and all(isinstance(v, int) and not isinstance(v, bool)
+                                                                for v in r) for r in board))
+
 
 class GpuSolverBackend:
-    """Kernels of one or more local GPUs (batches are sharded across them)."""
+    """Kernels of one or more local GPUs; a batch is split over `devices`.
+
+    Each entry of `devices` is one solver with its own workspace and its own
+    stream, so a device listed twice ([0, 0]) runs two solvers side by side
+    on one GPU (the first uses the process-wide solver of that device).  A
+    batch goes host -> pinned staging -> every solver's stream (copy in,
+    solve, copy out, all asynchronous), then one wait on all of them: the
+    devices work at the same time.  A solver's op_lock is held only while
+    its launches are enqueued; the pass count of this batch comes from two
+    stream-ordered counter snapshots around the solve (sdk_snapshot_stats),
+    so another peer sharing the device neither interleaves with the bracket
+    nor leaks into the count, and nothing synchronises under the lock."""
 
     def __init__(self, devices=None):
         if devices is None:
             devices = [torch.cuda.current_device()] if torch.cuda.is_available() else [None]
-        solvers = {}
+        self.solvers = []
         for d in devices:
             s = get_solver(d)
-            solvers[s.device.index] = s
-        self.solvers = [solvers[k] for k in sorted(solvers)]  # lock order: device index
+            if any(t is s for t in self.solvers):
+                s = BatchSolver(s.device)  # another workspace on the same GPU
+            self.solvers.append(s)
+        # created once per solver: each stream takes one of the process's few
+        # hardware queues (solver.py solve_host)
+        self.streams = [torch.cuda.Stream(s.device) for s in self.solvers]
+        self._lock = threading.Lock()  # one batch at a time on these streams
 
     def solve(self, boards: torch.Tensor, order: str):
-        """(n,81) host boards -> (host solutions, host status, passes).  Each
-        device's op_lock is held from the pass-counter read before the launch
-        to the one after it, so other users of the device (another peer in
-        this process) neither interleave launches nor leak into the count."""
+        """(n,81) host boards -> (host solutions, host status, passes)."""
         boards = as_boards(boards)
         n = boards.shape[0]
-        k = len(self.solvers)
-        parts = [boards[i * n // k:(i + 1) * n // k] for i in range(k)]
-        for s in self.solvers:
-            s.op_lock.acquire()
-        try:
-            outs = []
-            for s, part in zip(self.solvers, parts):  # launches are asynchronous per device
-                if part.shape[0] == 0:
-                    outs.append(None)
-                    continue
-                before = s.stats()["sweeps"]
-                outs.append((s.solve(part, order=order), before))
-            sols, st, sweeps = [], [], 0
-            for s, o in zip(self.solvers, outs):
-                if o is None:
-                    continue
-                (sol, stt), before = o
-                sols.append(sol.cpu())
-                st.append(stt.cpu())
-                sweeps += s.stats()["sweeps"] - before
-        finally:
-            for s in reversed(self.solvers):
-                s.op_lock.release()
-        if not sols:
+        if n == 0:
             return torch.empty((0, 81), dtype=torch.uint8), torch.empty(0, dtype=torch.int32), 0
-        return torch.cat(sols), torch.cat(st), sweeps
+        k = len(self.solvers)
+        pin = torch.empty((n, 81), dtype=torch.uint8, pin_memory=True)
+        pin.copy_(boards)
+        out = torch.empty((n, 81), dtype=torch.uint8, pin_memory=True)
+        st = torch.empty(n, dtype=torch.int32, pin_memory=True)
+        counts = torch.zeros((k, 6), dtype=torch.int64, pin_memory=True)
+        events = []
+        with self._lock:
+            for i, (s, stream) in enumerate(zip(self.solvers, self.streams)):
+                lo, hi = i * n // k, (i + 1) * n // k
+                if lo == hi:
+                    continue
+                with torch.cuda.device(s.device), torch.cuda.stream(stream):
+                    d_in = pin[lo:hi].to(s.device, non_blocking=True)
+                    d_out = torch.empty_like(d_in)
+                    d_st = torch.empty(hi - lo, dtype=torch.int32, device=s.device)
+                    with s.op_lock:  # enqueue only: snapshot, solve, snapshot in stream order
+                        before = s.stats_snapshot(stream)
+                        s.solve(d_in, out=d_out, status=d_st, order=order, stream=stream)
+                        after = s.stats_snapshot(stream)
+                    out[lo:hi].copy_(d_out, non_blocking=True)
+                    st[lo:hi].copy_(d_st, non_blocking=True)
+                    counts[i].copy_(after - before, non_blocking=True)
+                    ev = torch.cuda.Event()
+                    ev.record(stream)
+                    events.append(ev)
+            for ev in events:
+                ev.synchronize()
+        return out, st, int(counts[:, 3].sum())
 
     def peer_solve(self, boards: torch.Tensor):
-        """The reference's /solve loop per board (sdk_peer_solve_batch):
-        (boards it leaves, status, validations), on the host."""
-        out, st, val = self.solvers[0].peer_solve(as_boards(boards))
-        return out.cpu(), st.cpu(), val.cpu()
+        """The reference's /solve loop per board on a fresh node each
+        (sdk_peer_solve_batch): (boards it leaves, status, validations)."""
+        s, stream = self.solvers[0], self.streams[0]
+        with torch.cuda.device(s.device), torch.cuda.stream(stream):
+            out, st, val = s.peer_solve(as_boards(boards), stream=stream)
+            res = out.cpu(), st.cpu(), val.cpu()
+        return res
+
+    def new_peer_state(self):
+        """A new node's persistent /solve state (node.py:149, 167)."""
+        return self.solvers[0].new_peer_state()
+
+    def peer_solve_seq(self, boards: torch.Tensor, state):
+        """The reference's /solve loop on ONE node serving `boards` as
+        requests in order, from and into `state` (sdk_peer_solve_seq)."""
+        s, stream = self.solvers[0], self.streams[0]
+        with torch.cuda.device(s.device), torch.cuda.stream(stream):
+            out, st, val = s.peer_solve_seq(as_boards(boards), state, stream=stream)
+            res = out.cpu(), st.cpu(), val.cpu()
+        return res
 
     def check(self, boards, mode: int):
         return self.solvers[0].check(as_boards(boards, max_value=255), mode).cpu()
@@ -125,7 +181,13 @@ class BoardBatcher:
     "peer" for the reference's /solve loop) and returns a Future of
     (solutions, status); one thread drains the queue: it waits for the first
     board, then up to ``max_wait`` seconds (or until ``max_batch`` boards are
-    queued) for more, and solves each order's boards in one call."""
+    queued) for more, and solves each order's boards in one call.
+
+    "peer" boards are requests to this batcher's node, in arrival order:
+    they run as one sequence from the node's persistent /solve state
+    (``peer_state``: the reference P2PNode's partial_solution and
+    tried_numbers_by_position, node.py:149, 167), as the reference's
+    single-threaded HTTP server would take them one after the other."""
 
     def __init__(self, backend, max_batch: int = 1 << 16, max_wait: float = 0.0005, on_batch=None):
         self.backend = backend
@@ -138,6 +200,7 @@ class BoardBatcher:
         self._stop = False
         self.batches = 0
         self.boards = 0
+        self.peer_state = None  # created on the first "peer" batch
         self._thread = threading.Thread(target=self._run, name="BoardBatcher", daemon=True)
         self._thread.start()
 
@@ -154,6 +217,11 @@ class BoardBatcher:
             self._queued += boards.shape[0]
             self._cv.notify()
         return fut
+
+    def reset_peer_state(self):
+        """Forget the node's /solve state (a restarted reference node)."""
+        with self._cv:
+            self.peer_state = None
 
     def close(self):
         with self._cv:
@@ -191,7 +259,11 @@ class BoardBatcher:
                 try:
                     boards = torch.cat([it[0] for it in group])
                     if order == "peer":
-                        sols, st, val = self.backend.peer_solve(boards)
+                        with self._cv:
+                            if self.peer_state is None:
+                                self.peer_state = self.backend.new_peer_state()
+                            state = self.peer_state
+                        sols, st, val = self.backend.peer_solve_seq(boards, state)
                         passes = int(val.sum())
                     else:
                         sols, st, passes = self.backend.solve(boards, order)
@@ -208,6 +280,10 @@ class BoardBatcher:
                     for _, _, fut in group:
                         if not fut.done():
                             fut.set_exception(e)
+
+
+class PeerError(RuntimeError):
+    """A peer answered a forwarded board with an error."""
 
 
 class ReferenceNoReturn(RuntimeError):
@@ -328,7 +404,7 @@ class P2PNode:
     """node.py:134-657: UDP JSON peer + statistics; solving on local GPUs."""
 
     def __init__(self, host, port, anchor_node=None, handicap=0.001, backend=None,
-                 forward_threshold: Optional[int] = None, forward_timeout: float = 10.0,
+                 forward_threshold: Optional[int] = None, forward_timeout: float = 5.0,
                  max_wait: float = 0.0005, solve_mode: str = "walk"):
         if solve_mode not in ("walk", "reference"):
             raise ValueError("solve_mode must be 'walk' or 'reference'")
@@ -355,6 +431,8 @@ class P2PNode:
         self._task_ids = itertools.count(1)
         self._stats_timer = None
         self.lock = threading.RLock()
+        # UDP `solve` messages are served off the receive loop by a bounded pool
+        self._pool = ThreadPoolExecutor(max_workers=32, thread_name_prefix="udp-solve")
 
     # ---------------------------------------------------------- transport
     def send(self, address, msg):
@@ -420,7 +498,7 @@ class P2PNode:
     def handle_message(self, msg):
         t = msg.get("type")
         if t == "solve":  # GPU work off the receive loop
-            threading.Thread(target=self._handle_solve, args=(msg,), daemon=True).start()
+            self._pool.submit(self._handle_solve_safe, msg)
             return
         rebroadcast = False
         with self.lock:
@@ -488,15 +566,43 @@ class P2PNode:
             return True
         return False
 
+    def _handle_solve_safe(self, msg):
+        """Serve one UDP `solve`; whatever goes wrong, the requester gets a
+        `solution` with an `error` field instead of waiting for its timeout."""
+        try:
+            self._handle_solve(msg)
+        except Exception as e:  # noqa: BLE001 -- reported to the requester
+            logger.error("solve request failed: %s", e)
+            if isinstance(msg.get("address"), str):
+                reply = {"type": "solution", "error": str(e), "address": self.id}
+                if "task" in msg:
+                    reply["task"] = msg["task"]
+                for k in ("row", "col"):
+                    if k in msg:
+                        reply[k] = msg[k]
+                try:
+                    self.send(msg["address"], reply)
+                except OSError as e2:
+                    logger.error("could not report the failure to %s: %s", msg["address"], e2)
+
     def _handle_solve(self, msg):
         sudoku = msg.get("sudoku")
+        if not is_grid9(sudoku) and "sudokus" not in msg:
+            raise ValueError("sudoku must be 9 lists of 9 integers")
         if "row" in msg and "col" in msg:  # node.py:384-406: the cell task
             num = self.solver.solve_sudoku_destributed(sudoku, msg["row"], msg["col"])
             reply = {"type": "solution", "sudoku": sudoku, "row": msg["row"], "col": msg["col"],
                      "solution": num, "address": self.id}
         elif "sudokus" in msg:  # a batch handed over by a peer (81-character strings)
+            order = msg.get("order", "node")
+            if order not in BATCH_ORDERS:
+                raise ValueError(f"unknown order {order!r}")
+            if len(msg["sudokus"]) > MAX_UDP_BOARDS:
+                raise ValueError(f"more than {MAX_UDP_BOARDS} boards in one message")
+            if not all(isinstance(b, str) and len(b) == 81 and b.isdigit() for b in msg["sudokus"]):
+                raise ValueError("boards must be 81-digit strings")
             boards = torch.tensor([[int(c) for c in s] for s in msg["sudokus"]], dtype=torch.uint8).reshape(-1, 81)
-            sols, st = self.solver.solve_many(boards, order=msg.get("order", "node"))
+            sols, st = self.solver.solve_many(boards, order=order)
             with self.lock:
                 self.served += boards.shape[0]
             reply = {"type": "solution", "sudokus": ["".join(map(str, r.tolist())) for r in sols],
@@ -531,8 +637,19 @@ class P2PNode:
         return self._request(peer, msg, timeout)
 
     def request_solve_many(self, peer, boards81: List[str], order="node", timeout=10.0):
-        """Hand a batch of boards (81-character strings) to `peer`."""
-        return self._request(peer, {"type": "solve", "sudokus": list(boards81), "order": order}, timeout)
+        """Hand a batch of boards (81-character strings) to `peer`, in
+        messages of at most MAX_UDP_BOARDS boards; returns one reply with all
+        `sudokus` and `status` in order (or the first reply with an error)."""
+        boards81 = list(boards81)
+        sols, status = [], []
+        for lo in range(0, max(len(boards81), 1), MAX_UDP_BOARDS):
+            rep = self._request(peer, {"type": "solve", "sudokus": boards81[lo:lo + MAX_UDP_BOARDS],
+                                       "order": order}, timeout)
+            if rep.get("error"):
+                return rep
+            sols += rep["sudokus"]
+            status += rep["status"]
+        return {"type": "solution", "sudokus": sols, "status": status, "address": peer}
 
     def _request(self, peer, msg, timeout):
         tid = next(self._task_ids)
@@ -559,9 +676,15 @@ class P2PNode:
 
     def _reference_solve(self, board):
         """node.py:534-557 exactly (solve_mode "reference"): the greedy cell
-        loop on the GPU (sdk_peer_solve_batch).  Returns the board it leaves,
+        loop on the GPU (sdk_peer_solve_seq) from this node's persistent
+        state -- the reference P2PNode keeps partial_solution and
+        tried_numbers_by_position across requests (node.py:149, 167), so its
+        answer to a request can depend on the requests before it
+        (tests/golden/golden_peer_seq.json).  Returns the board it leaves,
         valid or not, and counts one solved puzzle either way (node.py:467-
-        474); raises ReferenceNoReturn where node.py never returns."""
+        474); raises ReferenceNoReturn where node.py never returns (the
+        reference node would spin forever; this one goes on serving from the
+        state the loop spun in)."""
         sols, st = self.solver.batcher.submit(as_boards(_flat(board)), "peer").result()
         if int(st[0]) == SDK_NO_RETURN:
             raise ReferenceNoReturn("the reference's /solve loop never returns on this board (node.py:429-464)")
@@ -583,6 +706,8 @@ class P2PNode:
         if peer is not None:
             try:
                 rep = self.request_solve(peer, board, timeout=self.forward_timeout, mode=mode)
+                if rep.get("error"):
+                    raise PeerError(rep["error"])
                 with self.lock:
                     self.forwarded += 1
                 self.broadcast_stats_soon()
@@ -592,8 +717,8 @@ class P2PNode:
                     _copy_into(board, _flat(rep["sudoku"]))
                     out = board
                 return out
-            except TimeoutError:
-                logger.warning("peer %s timed out, solving locally", peer)
+            except (TimeoutError, PeerError) as e:
+                logger.warning("peer %s failed (%s), solving locally", peer, e)
         try:
             if mode:
                 out = self._reference_solve(board)
@@ -602,6 +727,11 @@ class P2PNode:
         finally:
             self.broadcast_stats_soon()
         return out
+
+    def reset_solve_state(self):
+        """Forget the reference-mode /solve state (what restarting a
+        reference node does: a new P2PNode starts with both dicts empty)."""
+        self.solver.batcher.reset_peer_state()
 
     def get_stats(self):
         """node.py:598-620: {"all": {...}, "nodes": [...]} (plus "solved_by",
@@ -649,6 +779,7 @@ class P2PNode:
         self.broadcast_stats()
         self.broadcast({"type": "disconnect", "address": self.id})
         self.shutdown_flag = True
+        self._pool.shutdown(wait=False)
         self.solver.close()
 
 
@@ -676,7 +807,9 @@ class SudokuHTTPServer(BaseHTTPRequestHandler):
             return self._send_response({"error": "Invalid endpoint"}, 404)
         try:
             sudoku = json.loads(data.decode("utf-8"))["sudoku"]
-            as_boards(sudoku)  # shape / range validation
+            if not is_grid9(sudoku):
+                raise ValueError("sudoku must be 9 lists of 9 integers")
+            as_boards(sudoku)  # range validation
         except Exception as e:
             return self._send_response({"error": f"bad request: {e}"}, 400)
         t0 = time.time()

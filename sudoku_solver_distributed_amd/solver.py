@@ -217,6 +217,29 @@ class BatchSolver:
         _lib.check(rc, "sdk_peer_solve_batch")
         return out, st, val
 
+    def new_peer_state(self) -> torch.Tensor:
+        """A new P2PNode's persistent /solve state (partial_solution and
+        tried_numbers_by_position, node.py:149, 167) for peer_solve_seq."""
+        return torch.zeros(_lib.SDK_PEER_STATE_BYTES, dtype=torch.uint8, device=self.device)
+
+    def peer_solve_seq(self, boards, state: torch.Tensor, stream=None):
+        """The same /solve loop on ONE node serving the boards as requests in
+        order (sdk_peer_solve_seq): each request starts from the node state
+        the previous one left; `state` (new_peer_state()) is updated in place.
+        Returns (boards left, status, validations per request)."""
+        g = self._dev(as_boards(boards))
+        if state.device != self.device or state.dtype != torch.uint8 or state.numel() != _lib.SDK_PEER_STATE_BYTES:
+            raise ValueError("state must be a new_peer_state() tensor on this device")
+        n = g.shape[0]
+        out = torch.empty_like(g)
+        st = torch.empty(n, dtype=torch.int32, device=self.device)
+        val = torch.empty(n, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            rc = self.lib.sdk_peer_solve_seq(g.data_ptr(), out.data_ptr(), st.data_ptr(), val.data_ptr(), n,
+                                             state.data_ptr(), self._stream(stream))
+        _lib.check(rc, "sdk_peer_solve_seq")
+        return out, st, val
+
     def expand(self, nodes, order="gen", stream=None) -> torch.Tensor:
         """One frontier level (sdk_expand_frontier); synchronises to size it."""
         nd = self._dev(as_boards(nodes))
@@ -242,6 +265,17 @@ class BatchSolver:
         _lib.check(rc, "sdk_read_stats")
         return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4],
                 "deferred": out[5]}
+
+    def stats_snapshot(self, stream=None) -> torch.Tensor:
+        """The counters of stats() as a device int64 (6,) tensor, copied
+        asynchronously in stream order with this workspace's solves
+        (sdk_snapshot_stats): the difference of two snapshots around a solve
+        is that solve's own work, with no host synchronisation."""
+        out = torch.empty(6, dtype=torch.int64, device=self.device)
+        with self._lock, torch.cuda.device(self.device):
+            rc = self.lib.sdk_snapshot_stats(self.workspace.data_ptr(), out.data_ptr(), self._ws_stream(stream))
+        _lib.check(rc, "sdk_snapshot_stats")
+        return out
 
     # ------------------------------------------------------ frontier split
     def frontier(self, board, target: int = 4096, max_levels: int = 81, order="gen") -> torch.Tensor:

@@ -34,6 +34,15 @@ inputs + outputs as JSON data (no reference source is copied):
                          locally, node.py:443-449): README puzzle + gen boards.
                          Its answer can be partial or invalid; a 3 s alarm
                          records the boards on which it never returns.
+* golden_peer_seq.json -- the same /solve path on ONE node serving several
+                         requests in a row.  P2PNode keeps partial_solution
+                         and tried_numbers_by_position (node.py:149, 167)
+                         across requests (peer_sudoku_solve resets neither,
+                         node.py:534-552), so a later answer can depend on
+                         earlier ones; `fresh` is the answer of a new node,
+                         `validations` the node's counter after each request.
+                         A sequence ends at the first request the reference
+                         never returns from (the node would spin forever).
 """
 from __future__ import annotations
 
@@ -297,6 +306,41 @@ def main(ref_dir, stages):
         with open(os.path.join(HERE, "golden_peer.json"), "w") as f:
             json.dump(peer_cases, f, indent=0)
         print("peer", len(peer_cases))
+    # ----------------------------------------------------------- peer-seq
+    if "peerseq" in stages:
+        with open(os.path.join(HERE, "golden_peer.json")) as f:
+            fresh = {c["puzzle"]: c["returned"] for c in json.load(f)}
+        pool = [p for p, r in fresh.items() if r != "TIMEOUT"]
+        rng = random.Random(3)
+        seqs, differing, tries = [], 0, 0
+        while len(seqs) < 24 and tries < 2000:
+            tries += 1
+            k = rng.choice([2, 3, 4, 5])
+            boards = [rng.choice(pool) for _ in range(k)]
+            if rng.random() < 0.2:
+                boards[1] = boards[0]  # the same board twice in a row
+            steps = []
+            with contextlib.redirect_stdout(io.StringIO()):
+                n = node.P2PNode("127.0.0.1", 0, handicap=0)
+                for p in boards:
+                    try:
+                        out = run_limited(lambda: n.peer_sudoku_solve(b81(p)), 3)
+                        res = s81(out) if out else None
+                    except _Timeout:
+                        res = "TIMEOUT"
+                    steps.append({"puzzle": p, "returned": res, "fresh": fresh[p],
+                                  "validations": n.solver.validations,
+                                  "solved_puzzles": n.solver.solved_puzzles})
+                    if res == "TIMEOUT":
+                        break
+            d = any(st["returned"] != st["fresh"] for st in steps)
+            if not d and differing * 2 < len(seqs) + 1:
+                continue  # keep at least half the fixture on sequences where the state shows
+            differing += d
+            seqs.append({"requests": steps, "state_matters": d})
+        with open(os.path.join(HERE, "golden_peer_seq.json"), "w") as f:
+            json.dump(seqs, f, indent=0)
+        print("peerseq", len(seqs), "state matters in", differing, "tries", tries)
     print("done", stages)
 
 

@@ -32,6 +32,16 @@ class OracleBackend:
                 torch.tensor([code[r[0]] for r in res], dtype=torch.int32),
                 torch.tensor([r[2] for r in res], dtype=torch.int32))
 
+    def new_peer_state(self):
+        return O.PeerNode()
+
+    def peer_solve_seq(self, boards, node):
+        res = [node.solve(b) for b in boards.numpy()]
+        code = {1: 1, 0: 0, -1: -4}
+        return (torch.from_numpy(np.array([r[1] for r in res], dtype=np.uint8)),
+                torch.tensor([code[r[0]] for r in res], dtype=torch.int32),
+                torch.tensor([r[2] for r in res], dtype=torch.int32))
+
     def check(self, boards, mode):
         f = O.check if mode == 0 else O.check_sums
         return torch.tensor([int(f(b)) for b in boards.numpy()], dtype=torch.int32)
@@ -240,24 +250,45 @@ def test_two_peer_gpu_network_under_load():
 
 def _reference_mode_flow(backends):
     """solve_mode="reference": /solve answers exactly what the reference's
-    P2PNode.peer_sudoku_solve returned (tests/golden/golden_peer.json: board,
-    or no answer at all -> HTTP 500 here), validations counted like node.py,
-    and the same through a forwarding peer."""
+    P2PNode.peer_sudoku_solve returned -- on a fresh node (golden_peer.json;
+    the serving node's state is reset before each request) and along request
+    sequences on one node, whose partial_solution / tried sets carry over
+    (golden_peer_seq.json) -- with no answer at all (HTTP 500 here) where the
+    reference never returns, validations counted like node.py after every
+    request, and the same through a forwarding peer (the state is that of the
+    peer that serves the request)."""
     cases = load_golden("golden_peer.json")
+    seqs = load_golden("golden_peer_seq.json")
     nodes = _network(backends, forward={1: 0})
+    server = nodes[0][0]
     for n, _, _ in nodes:
         n.solve_mode = "reference"
+
+    def post(entry, puzzle, want):
+        code, body = _http(nodes[entry][2] + "/solve", {"sudoku": grid9(puzzle)})
+        if want == "TIMEOUT":
+            assert code == 500, puzzle
+        else:
+            assert code == 200 and "".join(str(v) for r in body for v in r) == want, puzzle
+
     try:
+        solved = 0
         for entry in (0, 1):  # peer 1 forwards every board to peer 0
             for c in cases:
-                code, body = _http(nodes[entry][2] + "/solve", {"sudoku": grid9(c["puzzle"])})
-                if c["returned"] == "TIMEOUT":
-                    assert code == 500, c["name"]
-                else:
-                    assert code == 200 and "".join(str(v) for r in body for v in r) == c["returned"], c["name"]
-        solved = sum(c["returned"] != "TIMEOUT" for c in cases)
-        assert nodes[0][0].solver.solved_puzzles == 2 * solved and nodes[1][0].forwarded == len(cases)
-        assert nodes[0][0].solver.validations == 2 * sum(c["validations"] for c in cases)
+                server.reset_solve_state()
+                v0 = server.solver.validations
+                post(entry, c["puzzle"], c["returned"])
+                assert server.solver.validations - v0 == c["validations"], c["name"]
+                solved += c["returned"] != "TIMEOUT"
+            for k, seq in enumerate(seqs):
+                server.reset_solve_state()
+                v0 = server.solver.validations
+                for r in seq["requests"]:
+                    post(entry, r["puzzle"], r["returned"])
+                    assert server.solver.validations - v0 == r["validations"], k
+                    solved += r["returned"] != "TIMEOUT"
+        assert server.solver.solved_puzzles == solved
+        assert nodes[1][0].forwarded == len(cases) + sum(len(q["requests"]) for q in seqs)
     finally:
         _shutdown(nodes)
 
@@ -270,3 +301,151 @@ def test_reference_solve_mode_cpu():
 def test_reference_solve_mode_gpu():
     from sudoku_solver_distributed_amd.node import GpuSolverBackend
     _reference_mode_flow([GpuSolverBackend([0]), GpuSolverBackend([0])])
+
+
+# ------------------------------------------------------------ protocol edges
+def _easy_boards(n):
+    return [c["puzzle"] for c in load_golden("golden_gen.json") if c["empty_boxes"] in (5, 20)][:n]
+
+
+def test_udp_solve_errors_are_answered():
+    """A `solve` the peer cannot serve is answered with an `error` at once
+    (no requester waits for its timeout): unknown order, malformed boards,
+    an oversized batch; request_solve_many splits big batches into messages
+    of at most MAX_UDP_BOARDS boards."""
+    from sudoku_solver_distributed_amd.node import MAX_UDP_BOARDS
+    nodes = _network([OracleBackend(), OracleBackend()])
+    a, b = nodes[0][0], nodes[1][0]
+    try:
+        t0 = time.monotonic()
+        rep = a._request(b.id, {"type": "solve", "sudokus": ["0" * 81], "order": "bogus"}, 5)
+        assert "unknown order" in rep["error"]
+        rep = a._request(b.id, {"type": "solve", "sudokus": ["12x" + "0" * 78]}, 5)
+        assert "81-digit" in rep["error"]
+        rep = a._request(b.id, {"type": "solve", "sudokus": ["0" * 81] * (MAX_UDP_BOARDS + 1)}, 5)
+        assert "more than" in rep["error"]
+        rep = a._request(b.id, {"type": "solve", "sudoku": [[0] * 9] * 8}, 5)
+        assert "9 lists" in rep["error"]
+        rep = a._request(b.id, {"type": "solve", "sudoku": [[0] * 9] * 9, "row": 0}, 5)  # no col: a whole board
+        assert rep["solved"]
+        assert time.monotonic() - t0 < 4
+        easy = _easy_boards(20)
+        boards = [easy[i % len(easy)] for i in range(2 * MAX_UDP_BOARDS + 7)]
+        rep = a.request_solve_many(b.id, boards, order="node")
+        want, wst = O.solve_batch(np.array([b81(x) for x in boards], dtype=np.uint8), order="node_literal")
+        assert rep["sudokus"] == ["".join(map(str, w)) for w in want] and rep["status"] == wst.tolist()
+        assert b.served == len(boards) + 1  # + the whole board above
+    finally:
+        _shutdown(nodes)
+
+
+def test_solve_rejects_what_is_not_a_board():
+    """POST /solve takes the reference's board type only (9 lists of 9
+    ints): a flat list, a string, 8 rows or a 10-wide row get HTTP 400."""
+    nodes = _network([OracleBackend()])
+    try:
+        url = nodes[0][2] + "/solve"
+        for bad in ([0] * 81, "0" * 81, [[0] * 9] * 8, [[0] * 10] + [[0] * 9] * 8, [[0.5] * 9] * 9,
+                    [[True] * 9] * 9):
+            code, body = _http(url, {"sudoku": bad})
+            assert code == 400 and "bad request" in body["error"], bad
+        code, _ = _http(url, {"sudoku": [[0] * 9] * 9})
+        assert code == 200
+    finally:
+        _shutdown(nodes)
+
+
+class _CountingBackend(OracleBackend):
+    """OracleBackend whose solve reports 7 passes per board."""
+
+    def solve(self, boards, order):
+        sols, st, _ = super().solve(boards, order)
+        return sols, st, 7 * boards.shape[0]
+
+
+def test_validations_semantics():
+    """check() / is_valid_move / the cell task add one
+    each (node.py:87); a walk solve adds the backend's propagation passes;
+    reference mode adds the reference's own count (test_reference_solve_mode_*)."""
+    from sudoku_solver_distributed_amd.node import SudokuSolver
+    s = SudokuSolver(0, backend=_CountingBackend())
+    try:
+        g = grid9(_easy_boards(1)[0])
+        assert s.validations == 0
+        s.check(g)
+        s.is_valid_move(g, 0, 0, 1)
+        s.solve_sudoku_destributed(g, 0, 0)
+        assert s.validations == 3
+        s.solve_sudoku([r[:] for r in g])
+        assert s.validations == 3 + 7
+        s.solve_many(torch.tensor([b81(x) for x in _easy_boards(5)], dtype=torch.uint8))
+        assert s.validations == 3 + 7 + 35
+    finally:
+        s.close()
+
+
+# ------------------------------------------------- configs[4] on the HIP path
+def _four_peer_gpu(forward):
+    from sudoku_solver_distributed_amd.node import GpuSolverBackend
+    # each peer backed by two solvers on the box's one MI355X: the shape of
+    # "2 MI355X per peer" (GpuSolverBackend splits every batch over both)
+    backends = [GpuSolverBackend([0, 0]) for _ in range(4)]
+    assert all(len(b.solvers) == 2 and b.solvers[0] is not b.solvers[1] for b in backends)
+    nodes = _network(backends, forward=forward)
+    try:
+        boards = _load_boards(1200)
+        t0 = time.monotonic()
+        answers = _load(nodes if forward is None else nodes[:1], boards, clients=64)
+        dt = time.monotonic() - t0
+        own = _check_network_run(nodes, boards, answers)
+        batches = sum(n[0].solver.batcher.batches for n in nodes)
+        print(f"4 peers x 2 solvers, forward={forward}: {len(boards) / dt:.0f} requests/s, {batches} GPU batches")
+        return nodes, own, batches
+    finally:
+        _shutdown(nodes)
+
+
+@pytest.mark.gpu
+def test_four_peer_gpu_network_under_load():
+    """configs[4] on the kernels: four peers, each GpuSolverBackend([0, 0])
+    (two workspaces / streams on one GPU: the multi-device branch), 1200
+    concurrent /solve requests from 64 clients over all four HTTP ports;
+    every answer is node.py's walk, /stats totals agree on every peer, and
+    the requests were coalesced into far fewer GPU batches."""
+    nodes, own, batches = _four_peer_gpu(None)
+    assert all(v > 0 for v in own.values()), own
+    assert batches < 1200 // 2, batches
+
+
+@pytest.mark.gpu
+def test_four_peer_gpu_forwarding():
+    """The same with every request entering at peer 0, which forwards all of
+    them (UDP solve / solution) to the other three GPU-backed peers."""
+    nodes, own, _ = _four_peer_gpu({0: 0})
+    assert nodes[0][0].forwarded == 1200 and own[nodes[0][0].id] == 0
+    assert sum(n[0].served for n in nodes[1:]) == 1200
+
+
+@pytest.mark.gpu
+def test_gpu_backend_split_and_pass_count():
+    """GpuSolverBackend([0, 0]) splits a batch over two solvers: same answers
+    as one solver, and the pass count it reports is exactly what the two
+    workspaces' counters grew by (walk-mode validations)."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    from sudoku_solver_distributed_amd.node import GpuSolverBackend, SudokuSolver
+    one, two = GpuSolverBackend([0]), GpuSolverBackend([0, 0])
+    boards = torch.cat([hard17_batch(3000, seed=5), torch.tensor([b81(x) for x in _load_boards(100)],
+                                                                  dtype=torch.uint8)])
+    s1, st1, p1 = one.solve(boards, "node")
+    before = [s.stats()["sweeps"] for s in two.solvers]
+    s2, st2, p2 = two.solve(boards, "node")
+    after = [s.stats()["sweeps"] for s in two.solvers]
+    assert torch.equal(s1, s2) and torch.equal(st1, st2)
+    assert p2 == sum(a - b for a, b in zip(after, before)) and p2 > len(boards)
+    node = SudokuSolver(0, backend=two)
+    try:
+        v0 = node.validations
+        node.solve_many(boards)
+        assert node.validations - v0 == p2
+    finally:
+        node.close()
