@@ -63,43 +63,54 @@ def _time(fn, reps=3):
     return best, out
 
 
-def node_load(dev, requests: int = 2000, clients: int = 32):
-    """BASELINE.json configs[4] serving figure: one in-process peer
-    (node.py mirror, GpuSolverBackend on this GPU) answering concurrent HTTP
-    POST /solve from `clients` client threads; requests/s and latency."""
+def node_load(dev, requests: int = 2000, clients: int = 32, peers: int = 1, solvers: int = 1):
+    """BASELINE.json configs[4] serving figure: `peers` in-process peers
+    (node.py mirror; each a GpuSolverBackend with `solvers` solvers on this
+    GPU -- the shape of "2 MI355X per peer" on one device) connected through
+    the first one, answering concurrent HTTP POST /solve from `clients`
+    client threads spread over their ports; requests/s and latency."""
     import urllib.request
     from concurrent.futures import ThreadPoolExecutor
 
     from sudoku_solver_distributed_amd.gen import hard17_batch
     from sudoku_solver_distributed_amd.node import GpuSolverBackend, P2PNode, make_http_server
-    node = P2PNode("127.0.0.1", 0, handicap=0, backend=GpuSolverBackend([dev.index]))
-    node.bind()
-    httpd = make_http_server(node, "127.0.0.1", 0)
-    threading.Thread(target=httpd.serve_forever, daemon=True).start()
-    url = f"http://127.0.0.1:{httpd.server_address[1]}/solve"
+    nodes, servers, urls = [], [], []
+    for i in range(peers):
+        node = P2PNode("127.0.0.1", 0, anchor_node=nodes[0].id if nodes else None, handicap=0,
+                       backend=GpuSolverBackend([dev.index] * solvers))
+        node.bind()
+        httpd = make_http_server(node, "127.0.0.1", 0)
+        threading.Thread(target=httpd.serve_forever, daemon=True).start()
+        threading.Thread(target=node.run, daemon=True).start()
+        nodes.append(node)
+        servers.append(httpd)
+        urls.append(f"http://127.0.0.1:{httpd.server_address[1]}/solve")
     boards = hard17_batch(requests, seed=77).numpy()
     bodies = [json.dumps({"sudoku": b.reshape(9, 9).tolist()}).encode() for b in boards]
 
     def one(i):
         t0 = time.perf_counter()
-        req = urllib.request.Request(url, data=bodies[i], headers={"Content-Type": "application/json"})
+        req = urllib.request.Request(urls[i % peers], data=bodies[i], headers={"Content-Type": "application/json"})
         with urllib.request.urlopen(req, timeout=60) as r:
             sol = json.loads(r.read())
         return time.perf_counter() - t0, sum(sum(row) for row in sol) == 405
     try:
         with ThreadPoolExecutor(max_workers=clients) as ex:
             list(ex.map(one, range(min(64, requests))))  # warm-up
-            b0 = node.solver.batcher.batches
+            b0 = sum(n.solver.batcher.batches for n in nodes)
             t0 = time.perf_counter()
             res = list(ex.map(one, range(requests)))
             el = time.perf_counter() - t0
         lat = sorted(r[0] for r in res)
-        return {"requests": requests, "clients": clients, "requests_per_s": requests / el,
+        return {"requests": requests, "clients": clients, "peers": peers, "solvers_per_peer": solvers,
+                "requests_per_s": requests / el,
                 "p50_ms": lat[len(lat) // 2] * 1e3, "p99_ms": lat[int(len(lat) * 0.99)] * 1e3,
-                "gpu_batches": node.solver.batcher.batches - b0, "all_solved": all(r[1] for r in res)}
+                "gpu_batches": sum(n.solver.batcher.batches for n in nodes) - b0,
+                "all_solved": all(r[1] for r in res)}
     finally:
-        node.shutdown()
-        httpd.shutdown()
+        for node, httpd in zip(nodes, servers):
+            node.shutdown()
+            httpd.shutdown()
 
 
 def e2e_rate(solver, boards, reps: int = 3):
@@ -140,7 +151,8 @@ def side_configs(solver, dev, world, rank, boards):
     configs[3]: one search-heavy board, the walk's direct single-wave solve
     vs the frontier split (over every rank's GPU when N > 1, RCCL
     all-reduce(MIN) early-exit word).
-    configs[4]: concurrent HTTP /solve against one peer (node_load).
+    configs[4]: concurrent HTTP /solve against one peer, and against four
+    peers with two solvers each (node_load).
     hard_search: 2^20 boards that need real search (gen.hard_search_batch).
     e2e: the timed batch with host buffers on both sides.
     Every result is checked.
@@ -167,6 +179,7 @@ def side_configs(solver, dev, world, rank, boards):
                               "deferred_per_call": s3["deferred"] / 3, "all_solved_and_checked": ok}
         out["e2e"] = e2e_rate(solver, boards)
         out["node_http"] = node_load(dev)
+        out["node_http_4peer"] = node_load(dev, requests=2000, clients=64, peers=4, solvers=2)
     board = torch.tensor([[int(c) for c in SEARCH_HEAVY]], dtype=torch.uint8, device=dev)
     t_direct, (g1, s1) = _time(lambda: solver.solve(board))
     st = {}
@@ -194,6 +207,12 @@ def main():
                     help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the configs[1] / configs[3] side measurements")
+    ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
+                    help="process group for N > 1 (nccl = RCCL, the product; gloo = rehearsal of the "
+                         "multi-rank path with every rank on one GPU)")
+    ap.add_argument("--device-index", type=int, default=None,
+                    help="put every rank on cuda:<index> instead of cuda:<LOCAL_RANK> (rehearsal of the "
+                         "multi-rank path on a one-GPU box)")
     args = ap.parse_args()
 
     import torch
@@ -204,10 +223,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
-    dev = torch.device("cuda", local)
+    gpu = local if args.device_index is None else args.device_index
+    torch.cuda.set_device(gpu)
+    dev = torch.device("cuda", gpu)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
+    comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
     from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
     from sudoku_solver_distributed_amd.solver import get_solver
@@ -243,7 +267,7 @@ def main():
     wall = time.perf_counter() - t0
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     st = solver.stats()
-    t = torch.tensor([wall], dtype=torch.float64, device=dev)
+    t = torch.tensor([wall], dtype=torch.float64, device=comm_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
@@ -340,7 +364,8 @@ def main():
         "config": {"workload": (f"hard 17-clue 9x9 batch, {args.batch} boards per GPU per step"
                                 if args.workload == "hard17" else
                                 f"search-heavy minimal 9x9 batch, {args.batch} boards per GPU per step"),
-                   "global_batch": args.batch * world, "parallelism": f"shard{world}"},
+                   "global_batch": args.batch * world, "parallelism": f"shard{world}",
+                   "dist_backend": args.dist_backend if world > 1 else None},
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,
         "guesses_per_board": st["guesses"] / max(st["finished"], 1),

@@ -19,3 +19,48 @@ def test_default_kernel_has_matching_pmc_profile():
     assert pmc["batch"] == 1 << 20 and pmc["seed"] == 2024
     assert pmc["valu_insts_per_launch"] > 0
     assert pmc["hbm_bytes_per_launch"] is None or pmc["hbm_bytes_per_launch"] > 0
+
+
+def _free_port():
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+import pytest  # noqa: E402
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_path_runs():
+    """bench.py's multi-rank path (barrier, max-time all-reduce, the side
+    configs' collectives, configs[3]'s split over ranks) executed once before
+    the driver's 8-GPU run does: two fresh bench processes, env rendezvous on
+    127.0.0.1, gloo, both ranks on cuda:0.  Rank 0 prints one JSON line."""
+    import subprocess
+    import sys
+    port = _free_port()
+    procs = []
+    for r in range(2):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE="2", LOCAL_WORLD_SIZE="2",
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(
+            [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
+             "--device-index", "0", "--steps", "2", "--warmup", "1", "--no-cpu", "--latency-boards", "4"],
+            cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = []
+    for p in procs:
+        try:
+            o, e = p.communicate(timeout=400)
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+        assert p.returncode == 0, e[-3000:]
+        outs.append(o)
+    lines = [l for l in outs[0].splitlines() if l.startswith("{")]
+    assert len(lines) == 1 and not [l for l in outs[1].splitlines() if l.startswith("{")]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 1 << 21 and d["config"]["dist_backend"] == "gloo"
+    assert d["side_configs"]["pathological"]["ranks"] == 2 and d["side_configs"]["pathological"]["identical"]
+    assert d["all_solved_and_checked"] and d["value"] > 0
