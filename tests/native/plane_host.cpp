@@ -255,3 +255,22 @@ extern "C" int64_t plane_check_pass(const uint8_t *in, int64_t n, int64_t nrand,
     }
     return bad;
 }
+
+// per-board pass and guess counts (scripts/drain_sim.py: the pass-count
+// distribution the plane kernel's scheduling sees)
+extern "C" void plane_board_passes(const uint8_t *in, int64_t n, int node_order, uint32_t *passes, uint32_t *guesses)
+{
+    static HostStack stk;
+    for (int64_t i = 0; i < n; ++i) {
+        uint32_t x[21];
+        words_of(in + i * 81, x);
+        plane::Board B;
+        bool clash = false;
+        passes[i] = guesses[i] = 0;
+        if (!plane::load_words(B, x, clash) || clash) continue;
+        plane::Stats st = {0, 0};
+        plane::solve(B, stk, node_order, 81, st);
+        passes[i] = st.passes;
+        guesses[i] = st.guesses;
+    }
+}
