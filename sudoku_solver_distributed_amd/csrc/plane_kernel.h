@@ -51,6 +51,21 @@
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
 #endif
+// 1: a claimed chunk is converted once, lane-parallel, into value bit-slice
+// records that refills hand out (plane_convert_chunk); 0: each refill stages
+// its boards and deposits them one at a time by ballots
+#ifndef SDK_PLANE_PRECONV
+#define SDK_PLANE_PRECONV 1
+#endif
+// 1: a push stores the board as 28 dwords from its own registers, 0: as
+// seven dwordx4 quads (built by copies: quads need aligned register tuples)
+#ifndef SDK_PLANE_PUSH_B32
+#define SDK_PLANE_PUSH_B32 0
+#endif
+// 1: a backtrack loads the level's whole stack line in one round trip
+#ifndef SDK_PLANE_POP1
+#define SDK_PLANE_POP1 1
+#endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
 // plus the loop iterations after the drain, into the second half of the
@@ -84,6 +99,13 @@ struct PlaneStack {
     __device__ __forceinline__ void push(uint32_t level, const plane::Board &B, uint32_t entry) const
     {
         const int v = (int)voff(level);
+#if SDK_PLANE_PUSH_B32
+        // 28 dword stores straight from the board's registers (no quad copies)
+#pragma unroll
+        for (int w = 0; w < 27; ++w) __builtin_amdgcn_raw_buffer_store_b32(B.P[w / 3][w % 3], rsrc, v, 4 * w, 0);
+        __builtin_amdgcn_raw_buffer_store_b32(entry, rsrc, v, 108, 0);
+        return;
+#endif
 #define PQ(a, b, c, d) (sdk_v4u){opaque(B.P[a / 3][a % 3]), opaque(B.P[b / 3][b % 3]), opaque(B.P[c / 3][c % 3]), \
                                  opaque(B.P[d / 3][d % 3])}
         const sdk_v4u q0 = PQ(0, 1, 2, 3), q1 = PQ(4, 5, 6, 7), q2 = PQ(8, 9, 10, 11), q3 = PQ(12, 13, 14, 15),
@@ -110,6 +132,29 @@ struct PlaneStack {
     __device__ __forceinline__ sdk_v4u top(uint32_t level) const
     {
         return __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)voff(level), 96, 0);
+    }
+    // the whole line in one round trip: the entry (last quad) decides whether
+    // the level still has a digit; if not (rare), the planes go unused
+    __device__ __forceinline__ sdk_v4u pop(uint32_t level, plane::Board &B) const
+    {
+        const int v = (int)voff(level);
+        const sdk_v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 0, 0);
+        const sdk_v4u q1 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 16, 0);
+        const sdk_v4u q2 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 32, 0);
+        const sdk_v4u q3 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 48, 0);
+        const sdk_v4u q4 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 64, 0);
+        const sdk_v4u q5 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 80, 0);
+        const sdk_v4u t = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 96, 0);
+        B.P[0][0] = q0.x; B.P[0][1] = q0.y; B.P[0][2] = q0.z; B.P[1][0] = q0.w;
+        B.P[1][1] = q1.x; B.P[1][2] = q1.y; B.P[2][0] = q1.z; B.P[2][1] = q1.w;
+        B.P[2][2] = q2.x; B.P[3][0] = q2.y; B.P[3][1] = q2.z; B.P[3][2] = q2.w;
+        B.P[4][0] = q3.x; B.P[4][1] = q3.y; B.P[4][2] = q3.z; B.P[5][0] = q3.w;
+        B.P[5][1] = q4.x; B.P[5][2] = q4.y; B.P[6][0] = q4.z; B.P[6][1] = q4.w;
+        B.P[6][2] = q5.x; B.P[7][0] = q5.y; B.P[7][1] = q5.z; B.P[7][2] = q5.w;
+        B.P[8][0] = t.x; B.P[8][1] = t.y; B.P[8][2] = t.z;
+        // all seven loads issued before the caller's branch on the entry
+        plane::pin_board(B);
+        return t;
     }
     __device__ __forceinline__ void restore(uint32_t level, plane::Board &B, const sdk_v4u &t) const
     {
@@ -260,6 +305,51 @@ __device__ __forceinline__ uint32_t plane_stage_span(const uint8_t *__restrict__
 __device__ __forceinline__ uint32_t lanes_below(uint64_t mask)
 {
     return __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0u));
+}
+
+// The 21 words of the board at byte offset o of the staging area (22 aligned
+// dword reads, funnel-shifted into place)
+__device__ __forceinline__ void plane_stage_words(const uint32_t *stage, uint32_t o, uint32_t (&x)[21])
+{
+    const uint32_t *d = stage + (o >> 2);
+    const uint32_t r = (o & 3u) * 8u;
+    uint32_t lo = d[0];
+#pragma unroll
+    for (int k = 0; k < 21; ++k) {
+        const uint32_t hi = d[k + 1];
+        x[k] = r ? __builtin_amdgcn_alignbit(hi, lo, r) : lo;
+        lo = hi;
+    }
+}
+
+// ---- chunk records
+// A claimed chunk (<= 64 consecutive boards) is staged once and converted
+// lane-parallel, a board per lane, into records of its value bit-slices:
+// V[s][b] at word 3s + b, word 12 = nonzero if a byte is > 9 (stride 13, odd:
+// 64 lanes writing / reading one word each hit 64 different banks).  A
+// refill then hands record i to the idle lane of rank i: every loaded lane
+// reads its own record at once, no per-board serial work.
+enum { PLANE_REC = 13 };
+static_assert(64 * PLANE_REC + 1 < PLANE_STAGE_DWORDS, "chunk records");
+
+__device__ __forceinline__ void plane_convert_chunk(uint32_t *stage, uint32_t sh, int count, int lane)
+{
+    uint32_t V[4][3], bad = 0;
+    if (lane < count) {
+        uint32_t x[21];
+        plane_stage_words(stage, sh + 81u * (uint32_t)lane, x);
+        bad = plane::slices_from_words(x, V);
+    }
+    // every lane's bytes are read (the loads above complete before their
+    // values are used) before any record overwrites them
+    if (lane < count) {
+        uint32_t *rec = stage + PLANE_REC * lane;
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) rec[3 * s + b] = V[s][b];
+        rec[12] = bad;
+    }
 }
 
 // ---- the store path's outbox
@@ -495,6 +585,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // refill (the head is one device-scope atomic for 4096 waves).  Chunks
     // shrink towards the end of the batch (guided: remaining / (2 waves)).
     int64_t res_lo = 0, res_hi = 0;
+    int64_t rec_base = 0;  // board of chunk record 0 (SDK_PLANE_PRECONV)
     bool queue_out = false;
     const int64_t nwaves = (int64_t)gridDim.x * (PLANE_THREADS / 64);
     uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
@@ -521,14 +612,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         if (q < n) {
             fin++;
             const uint8_t *src = puzzles + q * 81;
-            const uint8_t *sb = stage_b + sh + 81u * (uint32_t)lane;
             uint32_t x[21];
-#pragma unroll
-            for (int k = 0; k < 21; ++k) {
-                uint32_t w = sb[4 * k];
-                if (k < 20) w |= ((uint32_t)sb[4 * k + 1] << 8) | ((uint32_t)sb[4 * k + 2] << 16) | ((uint32_t)sb[4 * k + 3] << 24);
-                x[k] = w;
-            }
+            plane_stage_words(stage, sh + 81u * (uint32_t)lane, x);
             bool clash;  // tested lazily (see the unsolvable store above)
             const bool ok = plane::load_words(B, x, clash);
             const bool cancel = ok && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q;
@@ -646,6 +731,15 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     res_hi = res_lo + c < n ? res_lo + c : n;
                     if (res_lo > n) res_lo = n;
                     queue_out = res_lo + c >= n;
+#if SDK_PLANE_PRECONV
+                    // the whole chunk staged and converted once (chunk records)
+                    const int cc = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo));
+                    rec_base = res_lo;
+                    if (cc) {
+                        const uint32_t sh = plane_stage_span(puzzles, n, res_lo, cc, stage, lane);
+                        plane_convert_chunk(stage, sh, cc, lane);
+                    }
+#endif
                 }
                 base = (unsigned long long)res_lo;
                 // (wave-uniform: readfirstlane keeps the deposit loop a scalar loop)
@@ -656,6 +750,51 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 const uint64_t st_r1 = __builtin_amdgcn_s_memtime();
                 st_atom += st_r1 - st_r0;
 #endif
+#if SDK_PLANE_PRECONV
+                if (kk) {
+#if SDK_PLANE_STAMPS
+                    const uint64_t st_r2 = __builtin_amdgcn_s_memtime();
+#endif
+                    // idle lane of rank i < kk takes record base - rec_base + i
+                    const uint32_t rank = lanes_below(idle);
+                    const bool take = ((idle >> lane) & 1u) && rank < (uint32_t)kk;
+                    const uint64_t loaded = __builtin_amdgcn_ballot_w64(take);
+                    bool bad = false;
+                    if (take) {
+                        const uint32_t *rec = stage + PLANE_REC * ((uint32_t)(base - (unsigned long long)rec_base) + rank);
+                        uint32_t V[4][3], given[3];
+#pragma unroll
+                        for (int s = 0; s < 4; ++s)
+#pragma unroll
+                            for (int b = 0; b < 3; ++b) V[s][b] = rec[3 * s + b];
+                        bad = rec[12] != 0u;
+                        fin++;
+                        p = (int64_t)base + (int64_t)rank;
+                        depth = 0;
+                        bguess = 0;
+                        if (!bad && !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
+                            plane::planes_from_slices(B, V, given);
+                            state = PL_ACTIVE;
+                        } else {
+                            state = PL_CANCELLED;  // (bad: SDK_INVALID below)
+                        }
+                    }
+                    const uint64_t badm = __builtin_amdgcn_ballot_w64(bad);
+                    // boards with a byte > 9 (or cancelled): the raw input back
+                    uint64_t r = loaded & __builtin_amdgcn_ballot_w64(state != PL_ACTIVE);
+                    while (r) {
+                        const int i = __builtin_ctzll(r);
+                        r &= r - 1;
+                        const int64_t q = (int64_t)base + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
+                        plane_copy_board(puzzles + q * 81, sols + q * 81, lane);
+                        if (lane == 0) status[q] = ((badm >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
+                    }
+                    if (state == PL_CANCELLED) state = PL_IDLE;
+#if SDK_PLANE_STAMPS
+                    st_dep += __builtin_amdgcn_s_memtime() - st_r2;
+#endif
+                }
+#else
                 if (kk) {
                     const uint32_t sh = plane_stage_span(puzzles, n, (int64_t)base, kk, stage, lane);
 #if SDK_PLANE_STAMPS
@@ -730,6 +869,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     st_dep += __builtin_amdgcn_s_memtime() - st_r2;
 #endif
                 }
+#endif  // SDK_PLANE_PRECONV
             }
             // ---- tail: the queue is empty and the wave is down to a few
             // boards.  A pass costs the whole wave whatever its active
@@ -790,12 +930,20 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     break;
                 }
                 depth--;
+#if SDK_PLANE_POP1
+                const sdk_v4u t = stk.pop(depth, B);
+                const uint32_t e = t[3];
+                const uint32_t rem = (e >> 8) & 0x1FFu;
+                if (!rem) continue;
+                const uint32_t d = rem & (0u - rem);
+#else
                 const sdk_v4u t = stk.top(depth);
                 const uint32_t e = t[3];
                 const uint32_t rem = (e >> 8) & 0x1FFu;
                 if (!rem) continue;
                 const uint32_t d = rem & (0u - rem);
                 stk.restore(depth, B, t);
+#endif
                 B.Det[0] = B.Det[1] = B.Det[2] = 0;
                 stk.put_entry(depth, e & ~(d << 8));
                 depth++;

@@ -293,12 +293,14 @@ PS_FN uint32_t cell_cand(const Board &B, int band, int pos)
 // fix the cell at (band, pos) to the digit bit `dbit` (bit d = digit d+1)
 PS_FN void set_cell(Board &B, int band, int pos, uint32_t dbit)
 {
+    // one v_bitop3 per plane word: P & ~(cell-of-this-band & not-this-digit)
     const uint32_t cb = 1u << pos;
+    const uint32_t m[3] = {band == 0 ? cb : 0u, band == 1 ? cb : 0u, band == 2 ? cb : 0u};
 #pragma unroll
     for (int d = 0; d < 9; ++d) {
-        const uint32_t clr = ((dbit >> d) & 1u) ? 0u : cb;
+        const uint32_t other = ((dbit >> d) & 1u) - 1u;  // 0 for the digit, all ones otherwise
 #pragma unroll
-        for (int b = 0; b < 3; ++b) B.P[d][b] &= (b == band) ? ~clr : ~0u;
+        for (int b = 0; b < 3; ++b) B.P[d][b] = andn_and(B.P[d][b], m[b], other);
     }
 }
 
@@ -350,36 +352,67 @@ PS_FN bool givens_clash(const Board &B, const uint32_t (&given)[3])
     return bad != 0;
 }
 
+// sum of the byte products of a and b, plus c (v_dot4_u32_u8 on the GPU)
+PS_FN uint32_t dot4u8(uint32_t a, uint32_t b, uint32_t c)
+{
+#if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+    return __builtin_amdgcn_udot4(a, b, c, false);
+#else
+    for (int i = 0; i < 32; i += 8) c += ((a >> i) & 0xFFu) * ((b >> i) & 0xFFu);
+    return c;
+#endif
+}
+
+// Value bit-slices V[s][b] of a board given as 21 words x[k] = bytes
+// 4k..4k+3 (little endian; only byte 80 of x[20] is used).  Returns nonzero
+// if a byte is > 9.
+PS_FN uint32_t slices_from_words(const uint32_t (&x)[21], uint32_t (&V)[4][3])
+{
+    // Per value bit s, the 81-bit cell stream S (cell i = bit i) is built
+    // eight cells at a time: bit s of the 8 bytes of two words, gathered by
+    // one byte dot product each (weights 1, 2, 4, 8 and 16, 32, 64, 128 on
+    // bytes that are 0 or 2^s), lands 2^s times the 8-bit group; then the
+    // stream is cut into bands and the guard bits are inserted.  ~360 VALU
+    // per board where a per-cell shift / mask / or per bit takes ~1000.
+    const uint32_t x20 = x[20] & 0xFFu;
+    uint32_t hiset = 0;  // bits 4-7 of any byte: value >= 16
+#pragma unroll
+    for (int k = 0; k < 20; k += 2) hiset = or3(hiset, x[k], x[k + 1]);
+    hiset = (hiset | x20) & 0xF0F0F0F0u;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+        const uint32_t m = 0x01010101u << s;
+        uint32_t S[3] = {0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < 21; k += 2) {
+            const uint32_t lo = (k == 20 ? x20 : x[k]) & m;
+            uint32_t g = k < 20 ? dot4u8(x[k + 1] & m, 0x80402010u, 0u) : 0u;
+            g = dot4u8(lo, 0x08040201u, g);  // 2^s * cells 4k..4k+7
+            const int sh = (4 * k) % 32;     // 0, 8, 16, 24
+            S[k / 8] |= sh >= s ? g << (sh - s) : g >> (s - sh);
+        }
+        // cells 27b..27b+26, then a guard bit above each row of nine
+        const uint32_t c27[3] = {S[0] & 0x7FFFFFFu, ((S[0] >> 27) | (S[1] << 5)) & 0x7FFFFFFu,
+                                 (S[1] >> 22) | (S[2] << 10)};
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t w = c27[b];
+            V[s][b] = or3(w & 0x1FFu, (w << 1) & (0x1FFu << 10), (w << 2) & (0x1FFu << 20));
+        }
+    }
+    // a value of 10..15: bit 3 and bit 1 or 2
+    uint32_t big = 0;
+#pragma unroll
+    for (int b = 0; b < 3; ++b) big = or3(big, V[3][b] & V[1][b], V[3][b] & V[2][b]);
+    return hiset | big;
+}
+
 // Load from 21 words x[k] = bytes 4k..4k+3 of the board (little endian; only
 // byte 80 of x[20] is used).  Returns false if a byte is > 9.
 PS_FN bool load_words(Board &B, const uint32_t (&x)[21], bool &clash)
 {
-    uint32_t V[4][3] = {{0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}, {0u, 0u, 0u}};
-    uint32_t badb = 0;
-#pragma unroll
-    for (int k = 0; k < 21; ++k) {
-        const uint32_t w = k == 20 ? (x[k] & 0xFFu) : x[k];
-        badb |= ((w & 0x7F7F7F7Fu) + 0x76767676u | w) & 0x80808080u;  // some byte > 9
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int i = 4 * k + j;
-            if (i > 80) break;
-            const int b = cell_band(i), p = cell_pos(i);
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const int src = 8 * j + s;
-                const uint32_t bit = p >= src ? (w << (p - src)) : (w >> (src - p));
-                V[s][b] |= bit & (1u << p);
-            }
-        }
-        // one word at a time: unpinned, the OR chains of all 81 cells are
-        // re-associated into trees that keep every shifted term live
-#pragma unroll
-        for (int s = 0; s < 4; ++s)
-#pragma unroll
-            for (int b = 0; b < 3; ++b) PS_PIN(V[s][b]);
-        PS_PIN(badb);
-    }
+    uint32_t V[4][3];
+    const uint32_t badb = slices_from_words(x, V);
     uint32_t given[3];
     planes_from_slices(B, V, given);
     clash = badb == 0 && givens_clash(B, given);

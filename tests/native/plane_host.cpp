@@ -274,3 +274,4 @@ extern "C" void plane_board_passes(const uint8_t *in, int64_t n, int node_order,
         guesses[i] = st.guesses;
     }
 }
+

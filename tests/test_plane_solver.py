@@ -118,6 +118,8 @@ def test_plane_loader_matches_byte_loader(host):
     boards[1] = 0
     boards[2] = 9
     boards[3, 80] = 10
+    for v in range(10, 256):  # every invalid byte value, at positions of every word and byte lane
+        boards[100 + v, (7 * v) % 81] = v
     assert host.plane_check_load(boards.ctypes.data, n) == 0
 
 
