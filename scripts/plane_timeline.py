@@ -48,4 +48,18 @@ for k, name in ((4, "pass"), (5, "store+refill+control"), (8, "  of which queue 
                 (10, "  of which deposit"), (11, "  of which store"),
                 (6, "tail (wide / restart)")):
     print(f"  {name:22s} {st[:, k].sum() / cyc.sum():.3f} of stamped cycles, {st[:, k].mean() / 1e3:.1f} kcycles per wave")
+loop_end = us(st[:, 12])
+print("lane loop end pct", q, np.percentile(loop_end, q).round(1).tolist())
+print("post-drain lane phase us pct", q, np.percentile(loop_end - us(st[:, 1]), q).round(1).tolist())
+print("tail us pct", q, np.percentile(us(st[:, 2]) - loop_end, q).round(1).tolist())
+print("tail boards pct", q, np.percentile(st[:, 13], q).round(1).tolist(), " tail passes pct",
+      np.percentile(st[:, 14], q).round(1).tolist())
+late = us(st[:, 2]) >= np.percentile(us(st[:, 2]), 90)
+print(f"latest 10% of waves: drained at {us(st[late, 1]).mean():.1f} us (all: {us(st[:, 1]).mean():.1f}), "
+      f"lane phase {(loop_end - us(st[:, 1]))[late].mean():.1f} us, tail {(us(st[:, 2]) - loop_end)[late].mean():.1f} us, "
+      f"{st[late, 13].mean():.1f} boards / {st[late, 14].mean():.1f} passes")
+claims, last = st[:, 15] & 0xFFFFFFFF, st[:, 15] >> 32
+print(f"claims per wave mean {claims.mean():.1f}; last claim size: latest 10% {last[late].mean():.1f}, all {last.mean():.1f}")
+ld = us(st[:, 1]) >= np.percentile(us(st[:, 1]), 90)
+print(f"latest-drained 10% of waves: last claim size {last[ld].mean():.1f}, claims {claims[ld].mean():.1f}")
 print(f"  stamped kcycles per wave {cyc.mean() / 1e3:.1f} (shader clock; lifetime {life.mean():.1f} us)")

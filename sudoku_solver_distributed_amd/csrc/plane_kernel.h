@@ -37,7 +37,7 @@
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
 // $SDK_PLANE_TAIL, $SDK_PLANE_TAIL_MODE, $SDK_PLANE_CHUNK)
 #ifndef SDK_PLANE_REFILL
-#define SDK_PLANE_REFILL 6
+#define SDK_PLANE_REFILL 4
 #endif
 #ifndef SDK_PLANE_TAIL
 #define SDK_PLANE_TAIL 8
@@ -56,11 +56,6 @@
 // its boards and deposits them one at a time by ballots
 #ifndef SDK_PLANE_PRECONV
 #define SDK_PLANE_PRECONV 1
-#endif
-// 1: a push stores the board as 28 dwords from its own registers, 0: as
-// seven dwordx4 quads (built by copies: quads need aligned register tuples)
-#ifndef SDK_PLANE_PUSH_B32
-#define SDK_PLANE_PUSH_B32 0
 #endif
 // 1: a backtrack loads the level's whole stack line in one round trip
 #ifndef SDK_PLANE_POP1
@@ -99,13 +94,6 @@ struct PlaneStack {
     __device__ __forceinline__ void push(uint32_t level, const plane::Board &B, uint32_t entry) const
     {
         const int v = (int)voff(level);
-#if SDK_PLANE_PUSH_B32
-        // 28 dword stores straight from the board's registers (no quad copies)
-#pragma unroll
-        for (int w = 0; w < 27; ++w) __builtin_amdgcn_raw_buffer_store_b32(B.P[w / 3][w % 3], rsrc, v, 4 * w, 0);
-        __builtin_amdgcn_raw_buffer_store_b32(entry, rsrc, v, 108, 0);
-        return;
-#endif
 #define PQ(a, b, c, d) (sdk_v4u){opaque(B.P[a / 3][a % 3]), opaque(B.P[b / 3][b % 3]), opaque(B.P[c / 3][c % 3]), \
                                  opaque(B.P[d / 3][d % 3])}
         const sdk_v4u q0 = PQ(0, 1, 2, 3), q1 = PQ(4, 5, 6, 7), q2 = PQ(8, 9, 10, 11), q3 = PQ(12, 13, 14, 15),
@@ -598,6 +586,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     uint64_t st_pass = 0, st_io = 0, st_tail = 0, st_tb = 0;
     uint64_t st_atom = 0, st_dma = 0, st_dep = 0;  // parts of st_io: queue atomic, span DMA, per-board deposit
     uint64_t st_store = 0;                          // part of st_io: storing finished boards
+    uint64_t st_claims = 0;                         // queue claims: count | last size << 32
 #endif
 
     // Start-up: the wave's first 64 boards arrive as one staged span; each
@@ -721,11 +710,18 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 const uint64_t st_r0 = __builtin_amdgcn_s_memtime();
 #endif
                 if (res_lo == res_hi && !queue_out) {
-                    // guided chunk: this wave's share of what is left, at least k
+                    // guided chunk: this wave's share of what is left (as of its
+                    // own last claim), at least k.  Sizing by a fresh view of
+                    // the head (an agent-scope load of it, or a per-XCD hint
+                    // in L2) measured slower: more claims, each a span DMA and
+                    // a conversion, and all waves then drain at once
                     int64_t c = chunk > 0 ? (n - (res_hi > nt ? res_hi : nt)) / (2 * nwaves) : 0;
                     c = c > chunk ? chunk : c;
                     c = c < k ? k : c;
                     if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)c);
+#if SDK_PLANE_STAMPS
+                    st_claims = ((st_claims & 0xFFFFFFFFull) + 1) | ((uint64_t)c << 32);  // count, last size
+#endif
                     base = __shfl(base, leader);
                     res_lo = nt + (int64_t)base;
                     res_hi = res_lo + c < n ? res_lo + c : n;
@@ -957,6 +953,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     if (ob_count) plane_flush_outbox(outbox, ob_count, lane, sols);
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
+    const uint64_t st_t3 = __builtin_amdgcn_s_memrealtime();  // the lane loop ended
+    const uint32_t st_tailn = (uint32_t)__builtin_popcountll(tail_act);
+    uint32_t st_tailp = 0;
 #endif
     if (tail_act && tail_mode) {
         // ---- wave-wide tail: the lanes' boards go to LDS records (27 plane
@@ -978,6 +977,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         uint32_t wst[5];
         plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, puzzles, sols, status, ws, defer_list,
                         best, node_order, wst);
+#if SDK_PLANE_STAMPS
+        st_tailp = wst[2];
+#endif
         if (lane == 0) {
             solved += wst[0];
             guesses += wst[1];
@@ -1013,6 +1015,10 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         if (lane == 9) st[9] = (int64_t)st_dma;
         if (lane == 10) st[10] = (int64_t)st_dep;
         if (lane == 11) st[11] = (int64_t)st_store;
+        if (lane == 12) st[12] = (int64_t)st_t3;
+        if (lane == 13) st[13] = (int64_t)st_tailn;
+        if (lane == 14) st[14] = (int64_t)st_tailp;
+        if (lane == 15) st[15] = (int64_t)st_claims;
     }
 #endif
     // per-wave statistics: the lanes' counts summed, one atomic per counter and wave
