@@ -6,14 +6,20 @@ One process per GPU (torchrun for N > 1, RCCL for the barrier / max-time
 reduction only: boards are independent, each rank solves its own shard, no
 data-path collective).  A step = one sdk_solve_batch over the rank's batch
 of B boards (default 2^20 = BASELINE.json's "1M hard 17-clue" batch) already
-resident in HBM.  value = all ranks' boards / max-over-ranks wall time.
+resident in HBM.  Consecutive steps keep --inflight (default 2) launches in
+flight per GPU, each on its own stream and workspace
+(BatchSolver.solve_inflight), so a launch's drain overlaps the next one's
+start; `serial` reports the same steps back to back.  value = all ranks'
+boards / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line with the contract fields plus:
   roofline     -- the solve kernel against the INT32 VALU roofline (VALU
                   instructions per launch from the committed rocprofv3 PMC
-                  profile of this exact workload, duration measured live
-                  with HIP events on the launch stream) and, as `hbm`, its
-                  algorithmic bytes per launch against HBM;
+                  profile of this exact workload, over kernel_ms = the
+                  timed GPU region per launch, HIP events; launch_ms = a
+                  launch's own start-to-end span, overlapped with its
+                  neighbours, which rocprofv3's kernel trace reports) and,
+                  as `hbm`, its algorithmic bytes per launch against HBM;
   cpu_baseline -- the oracle's literal reference walk (gen.py:6-28 restated in
                   C, oracle/) on a time-bounded sample of the same boards, one
                   walk per host core (affinity, capped by $OMP_NUM_THREADS),
@@ -194,8 +200,8 @@ def side_configs(solver, dev, world, rank, boards):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 20, help="boards per GPU per step")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--workload", choices=("hard17", "hard_search"), default="hard17",
@@ -205,6 +211,11 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-boards", type=int, default=32,
                     help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="launches in flight per GPU (BatchSolver.solve_inflight: each on its own stream and "
+                         "workspace, so one launch's drain overlaps the next one's start); 1 = back to back")
+    ap.add_argument("--launch-events", action="store_true",
+                    help="also time each launch's own span with events on its slot stream (launch_ms)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the configs[1] / configs[3] side measurements")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -240,38 +251,58 @@ def main():
     # rank-local shard of synthetic hard boards (weak scaling: B per GPU)
     make = hard17_batch if args.workload == "hard17" else hard_search_batch
     boards = make(args.batch, seed=args.seed + rank, device=dev)
-    out = torch.empty_like(boards)
-    status = torch.empty(args.batch, dtype=torch.int32, device=dev)
+    m = max(1, args.inflight)
+    # one (solutions, status) buffer pair per launch slot: step i writes pair i % m
+    bufs = [(torch.empty_like(boards), torch.empty(args.batch, dtype=torch.int32, device=dev)) for _ in range(m)]
+    out, status = bufs[0]
     stream = torch.cuda.current_stream(dev)
+    solver._slot_solvers(m)  # slot workspaces allocated before any timing
 
-    for _ in range(args.warmup):
-        solver.solve(boards, out=out, status=status)
+    def steps(k, events=None):
+        solver.solve_inflight([boards] * k, [bufs[i % m][0] for i in range(k)], [bufs[i % m][1] for i in range(k)],
+                              inflight=m, launch_events=events)
+
+    steps(args.warmup)
     torch.cuda.synchronize(dev)
-    if not bool((status == 1).all()):
+    if not all(bool((bufs[i][1] == 1).all()) for i in range(min(m, args.warmup))):
         raise SystemExit("warmup: not every board solved")
 
-    solver.stats(reset=True)
+    solver.inflight_stats(reset=True)
     ev0 = torch.cuda.Event(enable_timing=True)
     ev1 = torch.cuda.Event(enable_timing=True)
+    launches = [] if args.launch_events else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
-        solver.solve(boards, out=out, status=status)
+    steps(args.steps, launches)
     ev1.record(stream)
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     wall = time.perf_counter() - t0
+    # the launches overlap (m in flight): a launch's share of the timed GPU
+    # region, and separately each launch's own start-to-end span
     kern_ms = ev0.elapsed_time(ev1) / args.steps
-    st = solver.stats()
+    launch_ms = sum(a.elapsed_time(b) for a, b in launches) / len(launches) if launches else None
+    st = solver.inflight_stats()
     t = torch.tensor([wall], dtype=torch.float64, device=comm_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
-    solved_ok = bool((status == 1).all()) and bool((solver.check(out, 0) == 1).all())
+    solved_ok = all(bool((bufs[i][1] == 1).all()) and bool((solver.check(bufs[i][0], 0) == 1).all())
+                    and bool(torch.equal(bufs[i][0], bufs[0][0])) for i in range(min(m, args.steps)))
+
+    # the same steps back to back (one launch in flight), for comparison
+    serial = None
+    if m > 1:
+        torch.cuda.synchronize(dev)
+        s0 = time.perf_counter()
+        solver.solve_inflight([boards] * args.steps, [out] * args.steps, [status] * args.steps, inflight=1)
+        torch.cuda.synchronize(dev)
+        s_wall = time.perf_counter() - s0
+        serial = {"value": args.batch * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3}
 
     # single-board latency (p50 over 32 boards, one launch each)
     lat = []
@@ -296,7 +327,7 @@ def main():
     value = total / wall_max
     kern_s = kern_ms / 1e3
     roof = {"bound": "valu", "achieved": None, "peak": PEAK_VALU_OPS / 1e12, "unit": "TOP/s",
-            "frac": None, "traffic": None, "kernel_ms": kern_ms,
+            "frac": None, "traffic": None, "kernel_ms": kern_ms, "launch_ms": launch_ms, "inflight": m,
             "hbm": {"achieved_GBps": BYTES_PER_BOARD * args.batch / kern_s / 1e9,
                     "peak_GBps": PEAK_HBM / 1e9,
                     "frac": BYTES_PER_BOARD * args.batch / kern_s / PEAK_HBM}}
@@ -365,7 +396,9 @@ def main():
                                 if args.workload == "hard17" else
                                 f"search-heavy minimal 9x9 batch, {args.batch} boards per GPU per step"),
                    "global_batch": args.batch * world, "parallelism": f"shard{world}",
+                   "inflight_per_gpu": m,
                    "dist_backend": args.dist_backend if world > 1 else None},
+        "serial": serial,
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,
         "guesses_per_board": st["guesses"] / max(st["finished"], 1),

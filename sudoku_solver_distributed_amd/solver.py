@@ -130,6 +130,61 @@ class BatchSolver:
         _lib.check(rc, "sdk_solve_batch")
         return out, status
 
+    def _slot_solvers(self, inflight: int):
+        """[self] + inflight - 1 more solvers on this device, each with its
+        own workspace (~1.1 GB: per-lane stacks) and its own stream."""
+        if not hasattr(self, "_slots"):
+            self._slots = [(self, torch.cuda.Stream(self.device))]
+        while len(self._slots) < inflight:
+            self._slots.append((BatchSolver(self.device), torch.cuda.Stream(self.device)))
+        return self._slots[:inflight]
+
+    def solve_inflight(self, batches, outs, statuses, inflight: int = 2, order="gen", ordered: bool = False,
+                       launch_events=None):
+        """Solve a sequence of device batches with up to `inflight` launches
+        in flight on this GPU: batch i runs on slot i % inflight (its own
+        workspace and stream), so a launch's end -- its last boards draining
+        while most lanes idle -- overlaps the next launch's start instead of
+        idling the GPU.  Each launch is a whole sdk_solve_batch; results are
+        those of solve().  outs[i] / statuses[i] receive batch i (buffers of
+        batches that may be in flight together must not alias).  The
+        caller's current stream waits for every batch; nothing synchronises
+        the host.  launch_events: optional list that receives a (start, end)
+        timing-event pair per batch, recorded on its slot's stream."""
+        if inflight < 1:
+            raise ValueError("inflight must be >= 1")
+        if not (len(batches) == len(outs) == len(statuses)):
+            raise ValueError("one out and one status tensor per batch")
+        slots = self._slot_solvers(inflight)
+        caller = torch.cuda.current_stream(self.device)
+        ready = torch.cuda.Event()
+        ready.record(caller)
+        for _, s in slots:
+            s.wait_event(ready)
+        for i, (b, o, st) in enumerate(zip(batches, outs, statuses)):
+            solver, s = slots[i % inflight]
+            if launch_events is not None:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record(s)
+            solver.solve(b, out=o, status=st, order=order, ordered=ordered, stream=s)
+            if launch_events is not None:
+                e1.record(s)
+                launch_events.append((e0, e1))
+            for t in (b, o, st):  # caller-stream allocations used on the slot's stream
+                if isinstance(t, torch.Tensor) and t.is_cuda:
+                    t.record_stream(s)
+        for _, s in slots:
+            caller.wait_stream(s)
+        return list(zip(outs, statuses))
+
+    def inflight_stats(self, reset: bool = False) -> dict:
+        """stats() summed over the solve_inflight slots' workspaces."""
+        tot = None
+        for solver, s in getattr(self, "_slots", [(self, None)]):
+            st = solver.stats(reset=reset, stream=s)
+            tot = st if tot is None else {k: (tot[k] + v if k != "best" else min(tot[k], v)) for k, v in st.items()}
+        return tot
+
     def solve_host(self, puzzles: torch.Tensor, order="gen", chunk: int = 1 << 18,
                    out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None
                    ) -> Tuple[torch.Tensor, torch.Tensor]:

@@ -511,3 +511,29 @@ def test_plane_refill_extremes(solver, refill, chunk):
     finally:
         lib.sdk_set_plane_tuning(-1, -1, -1, -1)
         lib.sdk_set_solve_kernel(prev)
+
+
+def test_solve_inflight_matches_solve(solver):
+    """Launches in flight on separate streams / workspaces (the bench's
+    steps): every batch's bytes and statuses equal solve()'s, batches of
+    different sizes and walk orders interleaved, counters summed over slots."""
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch, hard_search_batch
+    batches = [hard17_batch(40000, seed=5, device="cuda:0"), generate_batch(3000, 55, seed=6).cuda(),
+               hard_search_batch(20000, seed=7, device="cuda:0"), hard17_batch(9000, seed=8, device="cuda:0"),
+               generate_batch(50, 60, seed=9).cuda()]
+    for order in ("gen", "node"):
+        want = [solver.solve(b, order=order) for b in batches]
+        want = [(s.clone(), t.clone()) for s, t in want]
+        outs = [torch.empty_like(b) for b in batches]
+        sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in batches]
+        ev = []
+        solver.inflight_stats(reset=True)
+        got = solver.solve_inflight(batches, outs, sts, inflight=2, order=order, launch_events=ev)
+        torch.cuda.synchronize()
+        for (ws, wt), (gs, gt) in zip(want, got):
+            assert torch.equal(ws, gs) and torch.equal(wt, gt)
+        assert len(ev) == len(batches)
+        st = solver.inflight_stats()
+        assert st["finished"] == sum(b.shape[0] for b in batches)
+    with pytest.raises(ValueError):
+        solver.solve_inflight(batches, outs[:1], sts, inflight=2)
