@@ -39,3 +39,45 @@ for m in (1, 2, 1, 2):
     ok = all(bool((sts[k] == 1).all()) for k in range(m))
     print(f"in flight {m}: {ms:.3f} ms/step, {n / ms / 1e6:.3f} G boards/s, all solved {ok}", flush=True)
 print("outputs identical:", bool(torch.equal(outs[0], outs[1])))
+
+# the same through BatchSolver.solve_inflight (the bench's path)
+solver = solvers[0]
+solver._slots = [(solvers[0], streams[0]), (solvers[1], streams[1])]
+
+
+def run_api(m):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    solver.solve_inflight([boards] * steps, [outs[i % m] for i in range(steps)], [sts[i % m] for i in range(steps)],
+                          inflight=m)
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+for m in (1, 2, 1, 2):
+    run_api(m)
+    ms = run_api(m) * 1e3
+    print(f"solve_inflight {m}: {ms:.3f} ms/step, {n / ms / 1e6:.3f} G boards/s", flush=True)
+
+
+def run_bench_like(m, stats=False, events=False):
+    if stats:
+        solver.inflight_stats(reset=True)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    if events:
+        e0.record(torch.cuda.current_stream())
+    solver.solve_inflight([boards] * steps, [outs[i % m] for i in range(steps)], [sts[i % m] for i in range(steps)],
+                          inflight=m)
+    if events:
+        e1.record(torch.cuda.current_stream())
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+for kw in ({}, {"stats": True}, {"events": True}, {"stats": True, "events": True}, {}):
+    ms = run_bench_like(2, **kw) * 1e3
+    print(f"bench-like {kw}: {ms:.3f} ms/step, {n / ms / 1e6:.3f} G boards/s", flush=True)
+    ms = run_bench_like(2, **kw) * 1e3
+    print(f"bench-like {kw} again: {ms:.3f} ms/step, {n / ms / 1e6:.3f} G boards/s", flush=True)

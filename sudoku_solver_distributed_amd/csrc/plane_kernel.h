@@ -37,7 +37,7 @@
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
 // $SDK_PLANE_TAIL, $SDK_PLANE_TAIL_MODE, $SDK_PLANE_CHUNK)
 #ifndef SDK_PLANE_REFILL
-#define SDK_PLANE_REFILL 4
+#define SDK_PLANE_REFILL 3
 #endif
 #ifndef SDK_PLANE_TAIL
 #define SDK_PLANE_TAIL 8
@@ -546,7 +546,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     uint32_t *outbox = outbox_lds[threadIdx.x >> 6];
     uint32_t ob_count = 0;  // boards waiting in the outbox (wave-uniform)
+#if !SDK_PLANE_PRECONV
     const uint8_t *stage_b = (const uint8_t *)stage;
+#endif
     if ((threadIdx.x & 63) == 0) stage[PLANE_STAGE_DWORDS - 1] = 0u;  // the zero byte
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
