@@ -65,5 +65,6 @@ int sdk_plane_blocks_per_cu()
     int nb = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, plane_kernel, PLANE_THREADS, 0) != hipSuccess || nb <= 0)
         nb = 4;
-    return nb > 8 ? 8 : nb;
+    const int cap = 32 * 64 / PLANE_THREADS;  // 32 waves per CU
+    return nb > cap ? cap : nb;
 }
