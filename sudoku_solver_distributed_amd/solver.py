@@ -82,7 +82,7 @@ class BatchSolver:
         self._last_stream = None
         # held by callers that need solve + stats as one step (node.py's backend)
         self.op_lock = threading.RLock()
-        self._copy_streams = None  # solve_host's copy-in / copy-out streams
+        self._pool = None  # the solver's streams (_stream_pool)
         with torch.cuda.device(self.device):
             self.workspace = torch.zeros(int(self.lib.sdk_workspace_bytes()), dtype=torch.uint8,
                                          device=self.device)
@@ -130,13 +130,26 @@ class BatchSolver:
         _lib.check(rc, "sdk_solve_batch")
         return out, status
 
+    def _stream_pool(self, k: int):
+        """The solver's own streams, created once and shared by solve_host
+        (compute, copy-in, copy-out) and solve_inflight (one per slot): a
+        process has few hardware queues (4), and streams past them share a
+        queue and serialise, so the solver keeps to three besides the
+        caller's."""
+        if self._pool is None:
+            self._pool = []
+        while len(self._pool) < k:
+            self._pool.append(torch.cuda.Stream(self.device))
+        return self._pool[:k]
+
     def _slot_solvers(self, inflight: int):
         """[self] + inflight - 1 more solvers on this device, each with its
         own workspace (~1.1 GB: per-lane stacks) and its own stream."""
+        streams = self._stream_pool(inflight)
         if not hasattr(self, "_slots"):
-            self._slots = [(self, torch.cuda.Stream(self.device))]
+            self._slots = [(self, streams[0])]
         while len(self._slots) < inflight:
-            self._slots.append((BatchSolver(self.device), torch.cuda.Stream(self.device)))
+            self._slots.append((BatchSolver(self.device), streams[len(self._slots)]))
         return self._slots[:inflight]
 
     def solve_inflight(self, batches, outs, statuses, inflight: int = 2, order="gen", ordered: bool = False,
@@ -211,13 +224,12 @@ class BatchSolver:
         d_in = torch.empty((n, 81), dtype=torch.uint8, device=self.device)
         d_out = torch.empty_like(d_in)
         d_st = torch.empty(n, dtype=torch.int32, device=self.device)
-        compute = torch.cuda.current_stream(self.device)
-        if self._copy_streams is None:
-            # created once: each new stream takes a hardware queue slot, and
-            # past the process's few queues streams share them (and serialise)
-            self._copy_streams = (torch.cuda.Stream(self.device), torch.cuda.Stream(self.device))
-        h2d, d2h = self._copy_streams
-        h2d.wait_stream(compute)  # the device buffers are compute-stream allocations
+        caller = torch.cuda.current_stream(self.device)
+        # the solver's own three streams (created once: past the process's
+        # few hardware queues, streams share one and serialise)
+        compute, h2d, d2h = self._stream_pool(3)
+        compute.wait_stream(caller)
+        h2d.wait_stream(caller)  # the device buffers are caller-stream allocations
         for lo in range(0, n, chunk):
             hi = min(n, lo + chunk)
             with torch.cuda.stream(h2d):
@@ -231,6 +243,7 @@ class BatchSolver:
         for t in (d_in, d_out, d_st):
             t.record_stream(h2d)
             t.record_stream(d2h)
+            t.record_stream(compute)
         d2h.synchronize()
         return out, status
 
