@@ -13,5 +13,6 @@ timeout -k 10 300 python -u bench.py > gpurun_out/bench.json 2> gpurun_out/bench
 rc=$?; tail -c 600 gpurun_out/bench.json; step bench $rc
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_trace -o run --output-format csv -- python -u bench.py --no-cpu --no-extras --latency-boards 0 > gpurun_out/prof_trace.log 2>&1
 step trace $?
+python scripts/trace_summary.py gpurun_out/prof_trace/run_kernel_trace.csv gpurun_out/trace_summary.json > /dev/null
 bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1
 step pmc $?
