@@ -57,10 +57,6 @@
 #ifndef SDK_PLANE_PRECONV
 #define SDK_PLANE_PRECONV 1
 #endif
-// issue priority of a wave until it has drained (then 0); 0: all equal
-#ifndef SDK_PLANE_PRIO
-#define SDK_PLANE_PRIO 0
-#endif
 // 1: a backtrack loads the level's whole stack line in one round trip
 #ifndef SDK_PLANE_POP1
 #define SDK_PLANE_POP1 1
@@ -572,9 +568,6 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     uint32_t bguess = 0;  // guesses on the current board (dropped if it is handed off)
     bool drained = false;  // the queue is empty and this wave's reservoir too
-#if SDK_PLANE_PRIO
-    __builtin_amdgcn_s_setprio(SDK_PLANE_PRIO);
-#endif
     // Board hand-out.  The first nt boards go out statically, 64 consecutive
     // ones per wave; the rest through the queue head (board nt + head).  A
     // wave claims a CHUNK of boards at a time into its reservoir [res_lo,
@@ -751,12 +744,6 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 const int kk = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo < k ? res_hi - res_lo : k));
                 res_lo += kk;
                 drained = queue_out && res_lo == res_hi;
-#if SDK_PLANE_PRIO
-                // a drained wave steps its last boards with fewer and fewer
-                // lanes: it yields issue to the dense waves on its SIMD (the
-                // next launch in flight, or slower waves of this one)
-                if (drained) __builtin_amdgcn_s_setprio(0);
-#endif
 #if SDK_PLANE_STAMPS
                 const uint64_t st_r1 = __builtin_amdgcn_s_memtime();
                 st_atom += st_r1 - st_r0;

@@ -132,10 +132,9 @@ class BatchSolver:
 
     def _stream_pool(self, k: int):
         """The solver's own streams, created once and shared by solve_host
-        (compute, copy-in, copy-out) and solve_inflight (one per slot): a
-        process has few hardware queues (4), and streams past them share a
-        queue and serialise, so the solver keeps to three besides the
-        caller's."""
+        (compute, copy-in) and solve_inflight (one per slot): a process has
+        few hardware queues (4), and streams past them share a queue and
+        serialise."""
         if self._pool is None:
             self._pool = []
         while len(self._pool) < k:
@@ -225,9 +224,12 @@ class BatchSolver:
         d_out = torch.empty_like(d_in)
         d_st = torch.empty(n, dtype=torch.int32, device=self.device)
         caller = torch.cuda.current_stream(self.device)
-        # the solver's own three streams (created once: past the process's
-        # few hardware queues, streams share one and serialise)
-        compute, h2d, d2h = self._stream_pool(3)
+        # three streams in all: the solver's two (shared with solve_inflight's
+        # slots, created once) and the caller's for the copies out.  A
+        # process has few hardware queues (4); past them streams share one,
+        # and a copy queued behind a solve serialises the pipeline.
+        compute, h2d = self._stream_pool(2)
+        d2h = caller
         compute.wait_stream(caller)
         h2d.wait_stream(caller)  # the device buffers are caller-stream allocations
         for lo in range(0, n, chunk):
@@ -242,7 +244,6 @@ class BatchSolver:
                 status[lo:hi].copy_(d_st[lo:hi], non_blocking=True)
         for t in (d_in, d_out, d_st):
             t.record_stream(h2d)
-            t.record_stream(d2h)
             t.record_stream(compute)
         d2h.synchronize()
         return out, status
