@@ -183,6 +183,17 @@ def side_configs(solver, dev, world, rank, boards):
                               "guesses_per_board": s3["guesses"] / max(s3["finished"], 1),
                               "passes_per_board": s3["sweeps"] / max(s3["finished"], 1),
                               "deferred_per_call": s3["deferred"] / 3, "all_solved_and_checked": ok}
+        # the same batch as steps with two launches in flight (the headline's method)
+        k = 8
+        hb = [(torch.empty_like(hs), torch.empty(hs.shape[0], dtype=torch.int32, device=dev)) for _ in range(2)]
+        solver.solve_inflight([hs] * 2, [b[0] for b in hb], [b[1] for b in hb])
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        solver.solve_inflight([hs] * k, [hb[i % 2][0] for i in range(k)], [hb[i % 2][1] for i in range(k)])
+        torch.cuda.synchronize()
+        ti = (time.perf_counter() - t0) / k
+        out["hard_search"]["inflight"] = {"steps": k, "boards_per_s": hs.shape[0] / ti,
+                                          "identical": bool(torch.equal(hb[0][0], sols) and torch.equal(hb[1][0], sols))}
         out["e2e"] = e2e_rate(solver, boards)
         out["node_http"] = node_load(dev)
         out["node_http_4peer"] = node_load(dev, requests=2000, clients=64, peers=4, solvers=2)

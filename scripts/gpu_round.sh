@@ -16,3 +16,5 @@ step trace $?
 python scripts/trace_summary.py gpurun_out/prof_trace/run_kernel_trace.csv gpurun_out/trace_summary.json > /dev/null
 bash scripts/gpu_pmc.sh > gpurun_out/pmc.log 2>&1
 step pmc $?
+WORKLOAD=hard_search bash scripts/gpu_pmc.sh > gpurun_out/pmc_hs.log 2>&1
+step pmc_hard_search $?
