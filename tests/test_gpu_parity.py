@@ -537,3 +537,40 @@ def test_solve_inflight_matches_solve(solver):
         assert st["finished"] == sum(b.shape[0] for b in batches)
     with pytest.raises(ValueError):
         solver.solve_inflight(batches, outs[:1], sts, inflight=2)
+
+
+def test_chunk_records_invalid_and_clashing(solver):
+    """Boards that reach lanes through claimed chunks (past the static first
+    hand-out of one board per lane) come from the lane-parallel chunk-record
+    conversion: its invalid-byte flag (every value 10..255, in every byte
+    lane of a word), clashing givens (deferred to the wave kernel) and a
+    batch whose byte length is not a multiple of 4 -- statuses and bytes as
+    the oracle / the raw-input rule say."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    n = 300_001  # > one board per lane of the persistent grid; 81 n % 4 != 0
+    p = hard17_batch(n, seed=17).clone()
+    nt = solver.lib.sdk_plane_grid_lanes() if hasattr(solver.lib, "sdk_plane_grid_lanes") else 262_144
+    rng = np.random.default_rng(5)
+    bad_idx = rng.choice(np.arange(nt, n), size=246, replace=False)
+    for v, i in zip(range(10, 256), bad_idx):
+        p[i, (7 * v) % 81] = v
+    full = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
+    dup = "88" + full[2:30] + "0" + full[31:50] + "0" + full[51:70] + "0" + full[71:]
+    clash_idx = rng.choice(np.setdiff1d(np.arange(nt, n), bad_idx), size=40, replace=False)
+    for i in clash_idx:
+        p[i] = torch.tensor(b81(dup), dtype=torch.uint8)
+    p[n - 1] = torch.tensor(b81("0" * 81), dtype=torch.uint8)
+    sols, st = solver.solve(p.cuda())
+    sols, st = sols.cpu().numpy(), st.cpu().numpy()
+    pn = p.numpy()
+    assert (st[bad_idx] == -1).all() and np.array_equal(sols[bad_idx], pn[bad_idx])
+    want, wst = O.solve_batch(pn[clash_idx[:8]])
+    assert np.array_equal(st[clash_idx[:8]], wst) and np.array_equal(sols[clash_idx[:8]], want)
+    assert (st[clash_idx] == st[clash_idx[0]]).all()
+    want_last, wst_last = O.solve_batch(pn[n - 1:])
+    assert st[n - 1] == wst_last[0] and np.array_equal(sols[n - 1], want_last[0])
+    rest = np.setdiff1d(np.arange(n - 1), np.concatenate([bad_idx, clash_idx]))
+    assert (st[rest] == 1).all()
+    sample = rng.choice(rest, size=512, replace=False)
+    w, cnt = O.solve_unique_batch(pn[sample])
+    assert np.array_equal(sols[sample], w)
