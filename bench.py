@@ -211,7 +211,7 @@ def side_configs(solver, dev, world, rank, boards):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=1 << 20, help="boards per GPU per step")
     ap.add_argument("--seed", type=int, default=2024)
