@@ -574,3 +574,25 @@ def test_chunk_records_invalid_and_clashing(solver):
     sample = rng.choice(rest, size=512, replace=False)
     w, cnt = O.solve_unique_batch(pn[sample])
     assert np.array_equal(sols[sample], w)
+
+
+def test_chunk_records_ordered_mode(solver):
+    """Ordered mode (the frontier split's solve) on a batch large enough that
+    most boards arrive through chunk records: once board 0 is solved every
+    later board is either solved or cancelled with its input back, and the
+    lowest solved index is 0."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    n = 300_000
+    p = hard17_batch(n, seed=23)
+    solver.stats(reset=True)
+    sols, st = solver.solve(p.cuda(), ordered=True)
+    sols, st = sols.cpu().numpy(), st.cpu().numpy()
+    assert st[0] == 1 and solver.stats()["best"] == 0
+    assert set(np.unique(st).tolist()) <= {1, -2}
+    canc = np.nonzero(st == -2)[0]
+    assert np.array_equal(sols[canc], p.numpy()[canc])
+    done = np.nonzero(st == 1)[0]
+    rng = np.random.default_rng(3)
+    sample = rng.choice(done, size=min(256, len(done)), replace=False)
+    w, cnt = O.solve_unique_batch(p.numpy()[sample])
+    assert np.array_equal(sols[sample], w)
