@@ -1,2 +1,2 @@
 mkdir -p gpurun_out; export TMPDIR=/tmp
-timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 200 --timeout-method thread -m gpu -k "chunk_records or inflight or solve_host" > gpurun_out/t.log 2>&1; rc=$?; tail -5 gpurun_out/t.log; exit $rc
+BENCH_ARGS="--steps 50" CFGS="cur:default cur:SDK_PLANE_CHUNK=48 cur:SDK_PLANE_CHUNK=32 cur:SDK_PLANE_TAIL=6 cur:SDK_PLANE_TAIL=10 cur:SDK_PLANE_REFILL=2 cur:SDK_PLANE_REFILL=4" R=3 bash scripts/gpu_ab.sh || exit 1
