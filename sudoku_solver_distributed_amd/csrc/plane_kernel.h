@@ -13,9 +13,13 @@
 // the workspace (PlaneStack).  Finished lanes wait until at least
 // SDK_PLANE_REFILL lanes of the wave are free, then stores and refills run
 // once for all of them: solved boards go to the wave's LDS outbox (written
-// out 64 at a time, a board per lane, as dwords), new boards come in as one
-// staged span (wave-cooperative ballots).  Boards come from a static first
-// hand-out and then chunked claims on one queue head.
+// out 64 at a time, a board per lane, as dwords), new boards come from the
+// wave's chunk records in LDS (each claimed chunk staged as one span and
+// converted lane-parallel to value bit-slices once; a refilled lane reads
+// its record and builds its planes).  Boards come from a static first
+// hand-out and then chunked claims on one queue head.  A workgroup is one
+// wave: the waves share nothing, and a finished wave frees its LDS at once
+// for the next launch in flight (BatchSolver.solve_inflight).
 //
 // Once the queue is empty, a wave down to SDK_PLANE_TAIL boards hands them to
 // the wave-wide solver (plane_wide.h): each board in turn is spread over the
