@@ -539,6 +539,44 @@ def test_solve_inflight_matches_solve(solver):
         solver.solve_inflight(batches, outs[:1], sts, inflight=2)
 
 
+def test_solve_inflight_ragged_three_slots(solver):
+    """Three launches in flight over ragged batches -- empty, one board, an
+    invalid byte, clashing givens (the deferred kernel on a slot's own
+    workspace), an all-empty board -- equal solve()'s bytes and statuses;
+    ordered mode through the slots keeps each batch's own early-exit word."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    one = hard17_batch(1, seed=31)
+    bad = hard17_batch(700, seed=32).clone()
+    bad[3, 40] = 12
+    bad[5, 0], bad[5, 1] = 7, 7  # givens repeating a digit in a row
+    if bad[5, 2] == 7:
+        bad[5, 2] = 0
+    blank = torch.zeros((3, 81), dtype=torch.uint8)
+    batches = [b.cuda() for b in (torch.empty((0, 81), dtype=torch.uint8), one, bad, blank,
+                                  hard17_batch(30000, seed=33), one)]
+    want = [tuple(t.clone() for t in solver.solve(b)) for b in batches]
+    outs = [torch.empty_like(b) for b in batches]
+    sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in batches]
+    got = solver.solve_inflight(batches, outs, sts, inflight=3)
+    torch.cuda.synchronize()
+    for (ws, wt), (gs, gt) in zip(want, got):
+        assert torch.equal(ws, gs) and torch.equal(wt, gt)
+    st_bad = got[2][1].cpu().numpy()
+    assert st_bad[3] == -1 and np.array_equal(got[2][0][3].cpu().numpy(), bad[3].numpy())  # SDK_INVALID, input back
+    # ordered: board 0 of every batch solved, later ones solved or cancelled
+    # with their input back
+    big = [hard17_batch(20000, seed=40 + i).cuda() for i in range(3)]
+    outs = [torch.empty_like(b) for b in big]
+    sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in big]
+    got = solver.solve_inflight(big, outs, sts, inflight=3, ordered=True)
+    torch.cuda.synchronize()
+    for b, (s, t) in zip(big, got):
+        t = t.cpu().numpy()
+        assert t[0] == 1 and set(np.unique(t).tolist()) <= {1, -2}
+        canc = np.nonzero(t == -2)[0]
+        assert np.array_equal(s.cpu().numpy()[canc], b.cpu().numpy()[canc])
+
+
 def test_chunk_records_invalid_and_clashing(solver):
     """Boards that reach lanes through claimed chunks (past the static first
     hand-out of one board per lane) come from the lane-parallel chunk-record
