@@ -6,10 +6,11 @@ One process per GPU (torchrun for N > 1, RCCL for the barrier / max-time
 reduction only: boards are independent, each rank solves its own shard, no
 data-path collective).  A step = one sdk_solve_batch over the rank's batch
 of B boards (default 2^20 = BASELINE.json's "1M hard 17-clue" batch) already
-resident in HBM.  Consecutive steps keep --inflight (default 2) launches in
-flight per GPU, each on its own stream and workspace
-(BatchSolver.solve_inflight), so a launch's drain overlaps the next one's
-start; `serial` reports the same steps back to back.  value = all ranks'
+resident in HBM.  Consecutive steps keep --inflight (default 3) launches in
+flight per GPU, each on its own stream and workspace, each launch's grid
+holding --grid-waves (default 2) waves per SIMD (BatchSolver.solve_inflight):
+two launches are resident at once and a third fills the first one's drain;
+`serial` reports the same steps back to back on full grids.  value = all ranks'
 boards / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line with the contract fields plus:
@@ -183,17 +184,17 @@ def side_configs(solver, dev, world, rank, boards):
                               "guesses_per_board": s3["guesses"] / max(s3["finished"], 1),
                               "passes_per_board": s3["sweeps"] / max(s3["finished"], 1),
                               "deferred_per_call": s3["deferred"] / 3, "all_solved_and_checked": ok}
-        # the same batch as steps with two launches in flight (the headline's method)
-        k = 8
-        hb = [(torch.empty_like(hs), torch.empty(hs.shape[0], dtype=torch.int32, device=dev)) for _ in range(2)]
-        solver.solve_inflight([hs] * 2, [b[0] for b in hb], [b[1] for b in hb])
+        # the same batch as steps with launches in flight (the headline's method)
+        k, m = 9, 3
+        hb = [(torch.empty_like(hs), torch.empty(hs.shape[0], dtype=torch.int32, device=dev)) for _ in range(m)]
+        solver.solve_inflight([hs] * m, [b[0] for b in hb], [b[1] for b in hb], inflight=m)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        solver.solve_inflight([hs] * k, [hb[i % 2][0] for i in range(k)], [hb[i % 2][1] for i in range(k)])
+        solver.solve_inflight([hs] * k, [hb[i % m][0] for i in range(k)], [hb[i % m][1] for i in range(k)], inflight=m)
         torch.cuda.synchronize()
         ti = (time.perf_counter() - t0) / k
         out["hard_search"]["inflight"] = {"steps": k, "boards_per_s": hs.shape[0] / ti,
-                                          "identical": bool(torch.equal(hb[0][0], sols) and torch.equal(hb[1][0], sols))}
+                                          "identical": all(bool(torch.equal(b[0], sols)) for b in hb)}
         out["e2e"] = e2e_rate(solver, boards)
         out["node_http"] = node_load(dev)
         out["node_http_4peer"] = node_load(dev, requests=2000, clients=64, peers=4, solvers=2)
@@ -222,9 +223,12 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-boards", type=int, default=32,
                     help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
-    ap.add_argument("--inflight", type=int, default=2,
+    ap.add_argument("--inflight", type=int, default=3,
                     help="launches in flight per GPU (BatchSolver.solve_inflight: each on its own stream and "
-                         "workspace, so one launch's drain overlaps the next one's start); 1 = back to back")
+                         "workspace, so one launch's drain overlaps the next ones); 1 = back to back")
+    ap.add_argument("--grid-waves", type=int, default=-1,
+                    help="waves per SIMD in each launch's grid (sdk_solve_batch_grid; -1: solve_inflight's "
+                         "default, 2 with launches in flight, a full grid at --inflight 1; 0: a full grid)")
     ap.add_argument("--launch-events", action="store_true",
                     help="also time each launch's own span with events on its slot stream (launch_ms)")
     ap.add_argument("--no-extras", action="store_true",
@@ -268,10 +272,16 @@ def main():
     out, status = bufs[0]
     stream = torch.cuda.current_stream(dev)
     solver._slot_solvers(m)  # slot workspaces allocated before any timing
+    grid_waves = None if args.grid_waves < 0 else args.grid_waves
+    if grid_waves is None:
+        from sudoku_solver_distributed_amd.solver import GRID_WAVES_INFLIGHT
+        grid_waves_used = GRID_WAVES_INFLIGHT if m > 1 else 0
+    else:
+        grid_waves_used = grid_waves
 
     def steps(k, events=None):
         solver.solve_inflight([boards] * k, [bufs[i % m][0] for i in range(k)], [bufs[i % m][1] for i in range(k)],
-                              inflight=m, launch_events=events)
+                              inflight=m, launch_events=events, grid_waves=grid_waves)
 
     steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -407,7 +417,7 @@ def main():
                                 if args.workload == "hard17" else
                                 f"search-heavy minimal 9x9 batch, {args.batch} boards per GPU per step"),
                    "global_batch": args.batch * world, "parallelism": f"shard{world}",
-                   "inflight_per_gpu": m,
+                   "inflight_per_gpu": m, "grid_waves_per_simd": grid_waves_used or None,
                    "dist_backend": args.dist_backend if world > 1 else None},
         "serial": serial,
         "p50_single_ms": p50,

@@ -63,6 +63,18 @@ size_t sdk_workspace_bytes(void);
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status,
                     int64_t n, void *d_workspace, int order, int ordered, void *stream);
 
+/* sdk_solve_batch with the lane-per-board kernel's grid capped at
+ * `grid_waves` waves per SIMD (0: as many as fit, sdk_solve_batch's choice).
+ * For launches kept in flight on several streams, each with its own
+ * workspace (BatchSolver.solve_inflight): with a grid of 2 waves per SIMD two
+ * launches are resident together, so one launch's drain (its last boards,
+ * most lanes idle) runs beside the next one's start.  Results never depend on
+ * it; a negative value is a bad argument (-2).  Replaces the same reference
+ * walks as sdk_solve_batch (gen.py:6-28, node.py:62-74). */
+int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status,
+                         int64_t n, void *d_workspace, int order, int ordered, void *stream,
+                         int grid_waves);
+
 /* Batch Sudoku.check (mode 0, sudoku.py:119-140: every row, column and box
  * sums to 45 and holds 9 distinct values) or node.py's SudokuSolver.check
  * (mode 1, node.py:82-116: sums only).  d_ok[i] = 1/0. */

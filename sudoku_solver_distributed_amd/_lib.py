@@ -27,6 +27,7 @@ ORDERS = {"gen": SDK_ORDER_GEN, "node": SDK_ORDER_NODE}
 EXPORTS = (
     "sdk_workspace_bytes",
     "sdk_solve_batch",
+    "sdk_solve_batch_grid",
     "sdk_check_batch",
     "sdk_first_candidate_batch",
     "sdk_peer_solve_batch",
@@ -66,6 +67,8 @@ def load() -> ctypes.CDLL:
     L.sdk_workspace_bytes.argtypes = []
     L.sdk_solve_batch.restype = i32
     L.sdk_solve_batch.argtypes = [vp, vp, vp, i64, vp, i32, i32, vp]
+    L.sdk_solve_batch_grid.restype = i32
+    L.sdk_solve_batch_grid.argtypes = [vp, vp, vp, i64, vp, i32, i32, vp, i32]
     L.sdk_check_batch.restype = i32
     L.sdk_check_batch.argtypes = [vp, vp, i64, i32, vp]
     L.sdk_first_candidate_batch.restype = i32

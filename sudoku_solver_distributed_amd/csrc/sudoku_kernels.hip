@@ -528,8 +528,14 @@ size_t sdk_workspace_bytes(void)
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
                     void *d_workspace, int order, int ordered, void *stream)
 {
+    return sdk_solve_batch_grid(d_puzzles, d_solutions, d_status, n, d_workspace, order, ordered, stream, 0);
+}
+
+int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
+                         void *d_workspace, int order, int ordered, void *stream, int grid_waves)
+{
     if (n < 0 || (n > 0 && (!d_puzzles || !d_solutions || !d_status || !d_workspace)) ||
-        (order != SDK_ORDER_GEN && order != SDK_ORDER_NODE)) {
+        (order != SDK_ORDER_GEN && order != SDK_ORDER_NODE) || grid_waves < 0) {
         snprintf(g_err, sizeof g_err, "sdk_solve_batch: bad arguments (n=%lld)", (long long)n);
         return -2;
     }
@@ -557,7 +563,12 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
         hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
         // lanes: one per board up to a full grid; the stacks sit in the workspace
         const int64_t max_threads = plane_max_threads();
-        const int64_t threads = n < max_threads ? n : max_threads;
+        // grid_waves > 0: at most that many waves per SIMD (4 SIMDs per CU) in
+        // this launch's grid, so launches in flight on other streams are
+        // co-resident with it instead of queueing behind its drain
+        const int64_t grid_cap = (int64_t)cu_count() * 4 * grid_waves * 64;
+        const int64_t lane_cap = grid_waves > 0 && grid_cap < max_threads ? grid_cap : max_threads;
+        const int64_t threads = n < lane_cap ? n : lane_cap;
         uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
         int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
         e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, list, ordered, order, threads, st);

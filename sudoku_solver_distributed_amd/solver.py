@@ -67,6 +67,13 @@ def as_boards(x, device=None, max_value: int = 9) -> torch.Tensor:
     return t.contiguous()
 
 
+# waves per SIMD in each launch's grid when launches are in flight: a full
+# grid (4) leaves a launch's drain to the next launch only as its waves exit;
+# 2 keeps two launches resident together (measured +8 % at three
+# in flight over a full grid at two)
+GRID_WAVES_INFLIGHT = 2
+
+
 class BatchSolver:
     """One per device.  Holds the device workspace of the C ABI.
 
@@ -109,10 +116,13 @@ class BatchSolver:
 
     # -------------------------------------------------------------- solve
     def solve(self, puzzles, out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
-              ordered: bool = False, order="gen", stream=None) -> Tuple[torch.Tensor, torch.Tensor]:
+              ordered: bool = False, order="gen", stream=None, grid_waves: int = 0
+              ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Solve every board with the reference walk `order` ("gen":
         gen.py:6-28, "node": node.py:62-74).  Asynchronous on the stream;
-        returns (solutions uint8 (n,81), status int32 (n,))."""
+        returns (solutions uint8 (n,81), status int32 (n,)).  grid_waves > 0
+        caps the lane-per-board kernel's grid at that many waves per SIMD
+        (sdk_solve_batch_grid; solve_inflight's co-resident launches)."""
         p = self._dev(as_boards(puzzles))
         n = p.shape[0]
         if out is None:
@@ -124,10 +134,10 @@ class BatchSolver:
         if status.shape != (n,) or status.dtype != torch.int32:
             raise ValueError("status must be an (n,) int32 tensor")
         with self._lock, torch.cuda.device(self.device):
-            rc = self.lib.sdk_solve_batch(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
-                                          self.workspace.data_ptr(), _lib.order_code(order),
-                                          1 if ordered else 0, self._ws_stream(stream))
-        _lib.check(rc, "sdk_solve_batch")
+            rc = self.lib.sdk_solve_batch_grid(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
+                                               self.workspace.data_ptr(), _lib.order_code(order),
+                                               1 if ordered else 0, self._ws_stream(stream), int(grid_waves))
+        _lib.check(rc, "sdk_solve_batch_grid")
         return out, status
 
     def _stream_pool(self, k: int):
@@ -151,14 +161,16 @@ class BatchSolver:
             self._slots.append((BatchSolver(self.device), streams[len(self._slots)]))
         return self._slots[:inflight]
 
-    def solve_inflight(self, batches, outs, statuses, inflight: int = 2, order="gen", ordered: bool = False,
-                       launch_events=None):
+    def solve_inflight(self, batches, outs, statuses, inflight: int = 3, order="gen", ordered: bool = False,
+                       launch_events=None, grid_waves: Optional[int] = None):
         """Solve a sequence of device batches with up to `inflight` launches
         in flight on this GPU: batch i runs on slot i % inflight (its own
         workspace and stream), so a launch's end -- its last boards draining
-        while most lanes idle -- overlaps the next launch's start instead of
-        idling the GPU.  Each launch is a whole sdk_solve_batch; results are
-        those of solve().  outs[i] / statuses[i] receive batch i (buffers of
+        while most lanes idle -- overlaps the next launches instead of
+        idling the GPU.  grid_waves: waves per SIMD in each launch's grid
+        (default 2 with launches in flight -- two launches resident at once,
+        a third queued to fill the first one's drain; 0 = a full grid).  Each
+        launch is a whole sdk_solve_batch_grid; results are those of solve().  outs[i] / statuses[i] receive batch i (buffers of
         batches that may be in flight together must not alias).  The
         caller's current stream waits for every batch; nothing synchronises
         the host.  launch_events: optional list that receives a (start, end)
@@ -167,6 +179,8 @@ class BatchSolver:
             raise ValueError("inflight must be >= 1")
         if not (len(batches) == len(outs) == len(statuses)):
             raise ValueError("one out and one status tensor per batch")
+        if grid_waves is None:
+            grid_waves = GRID_WAVES_INFLIGHT if inflight > 1 else 0
         slots = self._slot_solvers(inflight)
         caller = torch.cuda.current_stream(self.device)
         ready = torch.cuda.Event()
@@ -178,7 +192,7 @@ class BatchSolver:
             if launch_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-            solver.solve(b, out=o, status=st, order=order, ordered=ordered, stream=s)
+            solver.solve(b, out=o, status=st, order=order, ordered=ordered, stream=s, grid_waves=grid_waves)
             if launch_events is not None:
                 e1.record(s)
                 launch_events.append((e0, e1))

@@ -97,3 +97,18 @@ def test_plane_tuning_arguments():
     assert f(8, 40, 0, 32) == 0
     assert f(-1, 0, -1, -1) == 0        # tail off
     assert f(-1, -1, -1, -1) == 0       # defaults back
+
+
+def test_solve_batch_grid_arguments():
+    """sdk_solve_batch_grid's argument check runs before any device call: a
+    negative grid is a bad argument (-2), an empty batch returns 0."""
+    from sudoku_solver_distributed_amd import _lib, build
+    build.build()
+    lib = ctypes.CDLL(_lib.LIB_PATH)
+    f = lib.sdk_solve_batch_grid
+    f.restype = ctypes.c_int
+    vp, i32 = ctypes.c_void_p, ctypes.c_int
+    f.argtypes = [vp, vp, vp, ctypes.c_int64, vp, i32, i32, vp, i32]
+    assert f(16, 16, 16, 1, 16, 0, 0, None, -1) == -2
+    assert f(None, None, None, 0, None, 0, 0, None, 2) == 0
+    assert f(None, None, None, 0, None, 7, 0, None, 2) == -2  # unknown order

@@ -577,6 +577,24 @@ def test_solve_inflight_ragged_three_slots(solver):
         assert np.array_equal(s.cpu().numpy()[canc], b.cpu().numpy()[canc])
 
 
+def test_grid_waves_same_results(solver):
+    """A launch's grid capped at 1 / 2 waves per SIMD (sdk_solve_batch_grid,
+    solve_inflight's co-resident launches) changes only how many lanes share
+    the batch: bytes and statuses equal the full grid's, in both orders, on a
+    batch several times the capped grid's lanes."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    p = torch.cat([hard17_batch(200_000, seed=51), hard_search_batch(60_000, seed=52)]).cuda()
+    p[7, 3] = 11  # an invalid byte past the static hand-out of the smallest grid
+    for order in ("gen", "node"):
+        want = [t.clone() for t in solver.solve(p, order=order)]
+        for gw in (1, 2):
+            got = solver.solve(p, order=order, grid_waves=gw)
+            torch.cuda.synchronize()
+            assert torch.equal(want[0], got[0]) and torch.equal(want[1], got[1]), (order, gw)
+    with pytest.raises(RuntimeError):
+        solver.solve(p[:1], grid_waves=-1)
+
+
 def test_chunk_records_invalid_and_clashing(solver):
     """Boards that reach lanes through claimed chunks (past the static first
     hand-out of one board per lane) come from the lane-parallel chunk-record
