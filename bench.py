@@ -4,14 +4,21 @@
 
 One process per GPU (torchrun for N > 1, RCCL for the barrier / max-time
 reduction only: boards are independent, each rank solves its own shard, no
-data-path collective).  A step = one sdk_solve_batch over the rank's batch
-of B boards (default 2^20 = BASELINE.json's "1M hard 17-clue" batch) already
-resident in HBM.  Consecutive steps keep --inflight (default 3) launches in
-flight per GPU, each on its own stream and workspace, each launch's grid
+data-path collective).  A step = the hot path over one batch of B boards
+(default 2^20 = BASELINE.json's "1M hard 17-clue" batch) already resident in
+HBM.  --scaling strong (the default; BASELINE configs[2]: "1M ... sharded
+across 1/2/4/8 MI355X"): B boards per step over ALL ranks, rank r solving
+its shard_bounds share (B/N boards) of every step's batch; weak: B boards per
+GPU per step.  A shard of a step too small to fill the GPU alone (2^17 boards
+at N = 8) is launched together with the rank's next steps' shards --
+sdk_solve_batches, one queue over up to 16 batches that drains once -- until a
+launch holds --launch-boards (2^20) boards; each step's shard keeps its own
+input and output buffers.  Consecutive launches keep --inflight (default 3)
+in flight per GPU, each on its own stream and workspace, each launch's grid
 holding --grid-waves (default 2) waves per SIMD (BatchSolver.solve_inflight):
 two launches are resident at once and a third fills the first one's drain;
-`serial` reports the same steps back to back on full grids.  value = all ranks'
-boards / max-over-ranks wall time.
+`serial` reports the same steps back to back on full grids.  value = all
+ranks' boards / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line with the contract fields plus:
   roofline     -- the solve kernel against the INT32 VALU roofline (VALU
@@ -120,6 +127,78 @@ def node_load(dev, requests: int = 2000, clients: int = 32, peers: int = 1, solv
             httpd.shutdown()
 
 
+def _free_ports(k: int):
+    import socket
+    socks, ports = [], []
+    for _ in range(k):
+        sk = socket.socket()
+        sk.bind(("127.0.0.1", 0))
+        socks.append(sk)
+        ports.append(sk.getsockname()[1])
+    for sk in socks:
+        sk.close()
+    return ports
+
+
+def node_load_procs(dev, peers: int = 4, solvers: int = 2, requests: int = 4000, clients: int = 64,
+                    load_procs: int = 4, startup_s: float = 240.0):
+    """BASELINE.json configs[4] in its process shape (README.md: one node.py
+    per peer): `peers` node.py processes (python -m
+    sudoku_solver_distributed_amd.node -h 0 --gpus <dev> x solvers; the
+    first is the others' anchor), and the HTTP load in `load_procs` more
+    processes (scripts/http_load.py).  Nothing of the bench process is on
+    the request path.  Requests/s, p50 / p99, every answer validated."""
+    import subprocess
+    import tempfile
+    import urllib.request
+    ports = _free_ports(2 * peers)
+    http, p2p = ports[:peers], ports[peers:]
+    procs, logs = [], []
+    try:
+        for i in range(peers):
+            cmd = [sys.executable, "-u", "-m", "sudoku_solver_distributed_amd.node", "-p", str(http[i]),
+                   "-s", str(p2p[i]), "-h", "0", "--gpus", ",".join([str(dev.index)] * solvers)]
+            if i:
+                cmd += ["-a", f"127.0.0.1:{p2p[0]}"]
+            log = tempfile.TemporaryFile(mode="w+")
+            logs.append(log)
+            procs.append(subprocess.Popen(cmd, cwd=ROOT, stdout=log, stderr=subprocess.STDOUT))
+        deadline = time.time() + startup_s
+        for i, p in enumerate(procs):  # each peer answers /stats
+            while True:
+                if p.poll() is not None:
+                    logs[i].seek(0)
+                    raise RuntimeError(f"peer {i} exited ({p.returncode}): {logs[i].read()[-1500:]}")
+                try:
+                    with urllib.request.urlopen(f"http://127.0.0.1:{http[i]}/stats", timeout=5) as r:
+                        r.read()
+                    break
+                except OSError:
+                    if time.time() > deadline:
+                        raise RuntimeError(f"peer {i} did not come up in {startup_s} s")
+                    time.sleep(0.5)
+        urls = [f"http://127.0.0.1:{h}/solve" for h in http]
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "http_load.py"), *urls,
+                            "--requests", str(requests), "--clients", str(clients), "--procs", str(load_procs)],
+                           cwd=ROOT, capture_output=True, text=True, timeout=600)
+        if r.returncode != 0:
+            raise RuntimeError(f"load generator failed: {r.stderr[-1500:]}")
+        res = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+        res.update({"peers": peers, "solvers_per_peer": solvers, "peer_processes": peers})
+        return res
+    finally:
+        for p in procs:
+            p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=20)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+        for log in logs:
+            log.close()
+
+
 def e2e_rate(solver, boards, reps: int = 3):
     """PCIe-inclusive rate: pinned host boards in, host solutions and
     statuses out (the serving path's view; `value` is device-resident).
@@ -149,9 +228,47 @@ def e2e_rate(solver, boards, reps: int = 3):
     return res
 
 
+def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
+    """configs[2]'s per-GPU regime under strong scaling, on one GPU: steps of
+    B/2, B/4, B/8 boards (a rank's shard of the B-board step at N = 2, 4, 8),
+    three launches in flight, either one step per launch (`ungrouped`) or
+    consecutive steps' shards in one sdk_solve_batches launch of
+    `launch_boards` boards (`grouped`, the bench's strong-scaling steps).
+    8 B boards per measurement, best of `reps`; every step checked SOLVED."""
+    import torch
+    n = boards.shape[0]
+    out = {}
+    for div in (2, 4, 8):
+        sh = n // div
+        parts = [boards[j * sh:(j + 1) * sh] for j in range(div)]
+        k = 8 * div
+        res = {"boards_per_step": sh, "steps": k}
+        for name, g in (("ungrouped", 1), ("grouped", max(1, min(16, -(-launch_boards // sh))))):
+            nb = 3 * max(g, div)
+            bufs = [(torch.empty_like(parts[0]), torch.empty(sh, dtype=torch.int32, device=boards.device))
+                    for _ in range(nb)]
+
+            def run(kk):
+                solver.solve_inflight([parts[i % div] for i in range(kk)], [bufs[i % nb][0] for i in range(kk)],
+                                      [bufs[i % nb][1] for i in range(kk)], inflight=3, group=g)
+            run(2 * g)
+            best = None
+            for _ in range(reps):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                run(k)
+                torch.cuda.synchronize()
+                el = time.perf_counter() - t0
+                best = el if best is None else min(best, el)
+            ok = all(bool((b[1] == 1).all()) for b in bufs[:min(nb, k)])
+            res[name] = {"steps_per_launch": g, "boards_per_s": sh * k / best, "all_solved": ok}
+        out[f"1/{div}"] = res
+    return out
+
+
 def side_configs(solver, dev, world, rank, boards):
-    """BASELINE.json configs[1], [3] and [4], a search-heavy batch and the
-    PCIe-inclusive rate, outside the timed region.
+    """BASELINE.json configs[1], [2]'s per-GPU shard regime, [3] and [4], a
+    search-heavy batch and the PCIe-inclusive rate, outside the timed region.
 
     configs[1]: 100k gen.py-style boards (generate_sudoku(50) under one seed,
     same random calls as gen.py:31-52) solved in one batch on one GPU.
@@ -168,6 +285,8 @@ def side_configs(solver, dev, world, rank, boards):
     from sudoku_solver_distributed_amd.distributed import solve_split
     from sudoku_solver_distributed_amd.gen import SEARCH_HEAVY, generate_batch, hard_search_batch
     out = {}
+    if rank == 0 and world == 1:
+        out["shard_rate"] = shard_rates(solver, boards)
     if rank == 0:
         gen = generate_batch(100_000, 50, seed=7, device=dev)
         t, (sols, st) = _time(lambda: solver.solve(gen))
@@ -196,8 +315,16 @@ def side_configs(solver, dev, world, rank, boards):
         out["hard_search"]["inflight"] = {"steps": k, "boards_per_s": hs.shape[0] / ti,
                                           "identical": all(bool(torch.equal(b[0], sols)) for b in hb)}
         out["e2e"] = e2e_rate(solver, boards)
+        # configs[4]: peers in THIS process (GIL-bound, labelled so) and
+        # peers as their own node.py processes (the reference's shape)
         out["node_http"] = node_load(dev)
         out["node_http_4peer"] = node_load(dev, requests=2000, clients=64, peers=4, solvers=2)
+        out["node_http_4peer"]["shape"] = "four peers and the client threads in the bench process"
+        for name, peers in (("node_http_1peer_procs", 1), ("node_http_4peer_procs", 4)):
+            try:
+                out[name] = node_load_procs(dev, peers=peers, solvers=2)
+            except Exception as e:  # a side figure: report, never fail the bench
+                out[name] = {"error": repr(e)[:800]}
     board = torch.tensor([[int(c) for c in SEARCH_HEAVY]], dtype=torch.uint8, device=dev)
     t_direct, (g1, s1) = _time(lambda: solver.solve(board))
     st = {}
@@ -214,7 +341,14 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--batch", type=int, default=1 << 20, help="boards per GPU per step")
+    ap.add_argument("--batch", type=int, default=1 << 20,
+                    help="boards per step: over all GPUs (--scaling strong) or per GPU (weak)")
+    ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
+                    help="strong: --batch boards per step sharded over the ranks (BASELINE configs[2]); "
+                         "weak: --batch boards per GPU per step")
+    ap.add_argument("--launch-boards", type=int, default=1 << 20,
+                    help="a launch solves consecutive steps' shards together (sdk_solve_batches, <= 16 steps) "
+                         "until it holds this many boards; 0 = one step per launch")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--workload", choices=("hard17", "hard_search"), default="hard17",
                     help="timed boards: BASELINE's hard 17-clue set (default, the metric's config) or the "
@@ -259,16 +393,36 @@ def main():
             dist.init_process_group("gloo")
     comm_dev = dev if args.dist_backend == "nccl" else torch.device("cpu")
 
+    from sudoku_solver_distributed_amd.distributed import shard_bounds
     from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
     from sudoku_solver_distributed_amd.solver import get_solver
 
     solver = get_solver(dev)
-    # rank-local shard of synthetic hard boards (weak scaling: B per GPU)
     make = hard17_batch if args.workload == "hard17" else hard_search_batch
-    boards = make(args.batch, seed=args.seed + rank, device=dev)
+    if args.scaling == "strong":
+        lo, hi = shard_bounds(args.batch, rank, world)
+    else:
+        lo, hi = 0, args.batch
+    shard = hi - lo  # this rank's boards per step
+    if shard <= 0:
+        raise SystemExit("--batch too small for the number of ranks")
+    # steps per launch: enough consecutive steps' shards to fill a launch
+    group = 1 if args.launch_boards <= shard else min(16, -(-args.launch_boards // shard))
+    # one input per step of a launch group (each step its own boards): step
+    # batch j is synthetic batch seed + 7919 j; strong: this rank's [lo, hi)
+    # of it (the same global batch on every rank), weak: per-rank seeds
+    inputs = []
+    for j in range(group):
+        sd = args.seed + 7919 * j + (rank if args.scaling == "weak" else 0)
+        full = make(args.batch, seed=sd)
+        inputs.append(full[lo:hi].contiguous().to(dev))
+        del full
+    boards = inputs[0]
     m = max(1, args.inflight)
-    # one (solutions, status) buffer pair per launch slot: step i writes pair i % m
-    bufs = [(torch.empty_like(boards), torch.empty(args.batch, dtype=torch.int32, device=dev)) for _ in range(m)]
+    # one (solutions, status) pair per step that can be in flight: step i
+    # reads inputs[i % group] and writes pair i % (m * group)
+    nb = m * group
+    bufs = [(torch.empty_like(boards), torch.empty(shard, dtype=torch.int32, device=dev)) for _ in range(nb)]
     out, status = bufs[0]
     stream = torch.cuda.current_stream(dev)
     solver._slot_solvers(m)  # slot workspaces allocated before any timing
@@ -279,13 +433,14 @@ def main():
     else:
         grid_waves_used = grid_waves
 
-    def steps(k, events=None):
-        solver.solve_inflight([boards] * k, [bufs[i % m][0] for i in range(k)], [bufs[i % m][1] for i in range(k)],
-                              inflight=m, launch_events=events, grid_waves=grid_waves)
+    def steps(k, events=None, inflight=m):
+        solver.solve_inflight([inputs[i % group] for i in range(k)], [bufs[i % nb][0] for i in range(k)],
+                              [bufs[i % nb][1] for i in range(k)], inflight=inflight, launch_events=events,
+                              grid_waves=grid_waves if inflight > 1 else 0, group=group)
 
     steps(args.warmup)
     torch.cuda.synchronize(dev)
-    if not all(bool((bufs[i][1] == 1).all()) for i in range(min(m, args.warmup))):
+    if not all(bool((bufs[i][1] == 1).all()) for i in range(min(nb, args.warmup))):
         raise SystemExit("warmup: not every board solved")
 
     solver.inflight_stats(reset=True)
@@ -312,18 +467,20 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
+    # every buffer a timed step wrote: all SOLVED, all pass Sudoku.check, and
+    # equal to the other buffers that hold the same input's answers
     solved_ok = all(bool((bufs[i][1] == 1).all()) and bool((solver.check(bufs[i][0], 0) == 1).all())
-                    and bool(torch.equal(bufs[i][0], bufs[0][0])) for i in range(min(m, args.steps)))
+                    and bool(torch.equal(bufs[i][0], bufs[i % group][0])) for i in range(min(nb, args.steps)))
 
     # the same steps back to back (one launch in flight), for comparison
     serial = None
     if m > 1:
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()
-        solver.solve_inflight([boards] * args.steps, [out] * args.steps, [status] * args.steps, inflight=1)
+        steps(args.steps, inflight=1)
         torch.cuda.synchronize(dev)
         s_wall = time.perf_counter() - s0
-        serial = {"value": args.batch * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3}
+        serial = {"value": shard * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3}
 
     # single-board latency (p50 over 32 boards, one launch each)
     lat = []
@@ -344,30 +501,38 @@ def main():
             dist.destroy_process_group()
         return
 
-    total = args.batch * world * args.steps
+    total = (args.batch if args.scaling == "strong" else args.batch * world) * args.steps
     value = total / wall_max
-    kern_s = kern_ms / 1e3
+    kern_s = kern_ms / 1e3  # this GPU's share of the timed region per step
+    shape = {"boards_per_step": shard, "group": group, "inflight": m, "grid_waves": grid_waves_used}
     roof = {"bound": "valu", "achieved": None, "peak": PEAK_VALU_OPS / 1e12, "unit": "TOP/s",
-            "frac": None, "traffic": None, "kernel_ms": kern_ms, "launch_ms": launch_ms, "inflight": m,
-            "hbm": {"achieved_GBps": BYTES_PER_BOARD * args.batch / kern_s / 1e9,
+            "frac": None, "traffic": None, "kernel_ms": kern_ms, "launch_ms": launch_ms, "shape": shape,
+            "hbm": {"achieved_GBps": BYTES_PER_BOARD * shard / kern_s / 1e9,
                     "peak_GBps": PEAK_HBM / 1e9,
-                    "frac": BYTES_PER_BOARD * args.batch / kern_s / PEAK_HBM}}
+                    "frac": BYTES_PER_BOARD * shard / kern_s / PEAK_HBM}}
     from sudoku_solver_distributed_amd import _lib
     kname = _lib.KERNEL_SYMBOLS.get(_lib.active_kernel(), "?")
+    if group > 1 and kname == "plane_kernel":
+        kname = "plane_kernel_multi"  # sdk_solve_batches' kernel
     roof["kernel"] = kname
     PMC_FILE = os.path.join(PMC_DIR, f"pmc_{kname}.json")
+    roof["pmc_match"] = False
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
             pmc = json.load(f)
-        if (pmc.get("batch") == args.batch and pmc.get("seed") == args.seed and pmc.get("kernel") == kname
-                and pmc.get("workload", "hard17") == args.workload):
-            ops = pmc["valu_insts_per_launch"] * 64
+        # the counters count only if they were taken on EXACTLY this launch
+        # shape (scripts/gpu_pmc.sh runs this bench with the same flags)
+        if (pmc.get("kernel") == kname and pmc.get("seed") == args.seed
+                and pmc.get("workload", "hard17") == args.workload and pmc.get("shape") == shape):
+            roof["pmc_match"] = True
+            valu_step = pmc["valu_insts_per_launch"] / group  # a launch is `group` steps
+            ops = valu_step * 64
             roof["achieved"] = ops / kern_s / 1e12
             roof["frac"] = roof["achieved"] / roof["peak"]
-            roof["valu_insts_per_launch"] = pmc["valu_insts_per_launch"]
+            roof["valu_insts_per_step"] = valu_step
             if pmc.get("hbm_bytes_per_launch") is not None:
-                roof["traffic"] = pmc["hbm_bytes_per_launch"]
-                roof["traffic_over_algorithmic"] = pmc["hbm_bytes_per_launch"] / (BYTES_PER_BOARD * args.batch)
+                roof["traffic"] = pmc["hbm_bytes_per_launch"] / group
+                roof["traffic_over_algorithmic"] = roof["traffic"] / (BYTES_PER_BOARD * shard)
             for k in ("sq_wait_inst_any_share", "sq_wait_any_share"):
                 if k in pmc:
                     roof[k] = pmc[k]
@@ -375,7 +540,7 @@ def main():
             # lanes doing pass work: passes x VALU per pass (ISA count of
             # plane::pass) over every lane slot the kernel issued
             isa = os.path.join(PMC_DIR, "isa_plane_pass.json")
-            if kname == "plane_kernel" and os.path.exists(isa):
+            if kname.startswith("plane_kernel") and os.path.exists(isa):
                 with open(isa) as f:
                     vpp = json.load(f)["valu_per_pass"]
                 useful = st["sweeps"] / args.steps * vpp
@@ -384,7 +549,7 @@ def main():
                 roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
             # the pass's own ceiling at the kernel's occupancy (microbenchmark)
             ceil = os.path.join(PMC_DIR, "r02_pass_ceiling.json")
-            if kname == "plane_kernel" and os.path.exists(ceil):
+            if kname.startswith("plane_kernel") and os.path.exists(ceil):
                 with open(ceil) as f:
                     c = json.load(f)
                 cp = c["by_waves_per_simd"][str(c["plane_kernel_waves_per_simd"])]["passes_per_s"]
@@ -409,17 +574,20 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": wall_max / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "u8",
-        "data": "synthetic: 17-clue unique-solution boards (symmetry images of certified seeds)",
-        "config": {"workload": (f"hard 17-clue 9x9 batch, {args.batch} boards per GPU per step"
-                                if args.workload == "hard17" else
-                                f"search-heavy minimal 9x9 batch, {args.batch} boards per GPU per step"),
-                   "global_batch": args.batch * world, "parallelism": f"shard{world}",
-                   "inflight_per_gpu": m, "grid_waves_per_simd": grid_waves_used or None,
+        "data": "synthetic: 17-clue unique-solution boards (symmetry images of 80 certified isomorphism "
+                "classes, data/hard17_classes.txt)" if args.workload == "hard17" else
+                "synthetic: search-heavy minimal boards (symmetry images of data/hard_search_seeds.txt)",
+        "config": {"workload": (f"{'hard 17-clue' if args.workload == 'hard17' else 'search-heavy minimal'} 9x9 "
+                                f"batch, {args.batch} boards per step "
+                                f"{'over all GPUs' if args.scaling == 'strong' else 'per GPU'}"),
+                   "global_batch": args.batch if args.scaling == "strong" else args.batch * world,
+                   "boards_per_gpu_per_step": shard, "parallelism": f"shard{world}",
+                   "steps_per_launch": group, "inflight_per_gpu": m, "grid_waves_per_simd": grid_waves_used or None,
                    "dist_backend": args.dist_backend if world > 1 else None},
-        "serial": serial,
+        "serial": serial,  # this GPU's steps back to back (rank 0's boards / s)
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,
         "guesses_per_board": st["guesses"] / max(st["finished"], 1),

@@ -75,6 +75,22 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
                          int64_t n, void *d_workspace, int order, int ordered, void *stream,
                          int grid_waves);
 
+/* Several independent batches solved by ONE launch sequence on one
+ * workspace (unordered): batch i is d_puzzles[i] -> d_solutions[i],
+ * d_status[i], n[i] boards, exactly as sdk_solve_batch_grid would solve it
+ * alone (same bytes, same statuses).  The lane-per-board kernel's queue runs
+ * over the batches laid end to end, so the lanes that finish one batch's
+ * boards take the next batch's and the grid drains once per call instead of
+ * once per batch: a multi-step persistent launch (bench.py's strong-scaling
+ * steps, where one GPU's share of a step is too small to fill the chip).
+ * 1 <= count <= SDK_MAX_BATCHES; a batch may be empty; batches must not
+ * overlap each other's outputs.  Returns 0 / -1 (HIP error) / -2 (bad
+ * arguments).  Replaces the same reference walks as sdk_solve_batch
+ * (gen.py:6-28, node.py:62-74), once per board. */
+#define SDK_MAX_BATCHES 16
+int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutions, int32_t *const *d_status,
+                      const int64_t *n, int count, void *d_workspace, int order, void *stream, int grid_waves);
+
 /* Batch Sudoku.check (mode 0, sudoku.py:119-140: every row, column and box
  * sums to 45 and holds 9 distinct values) or node.py's SudokuSolver.check
  * (mode 1, node.py:82-116: sums only).  d_ok[i] = 1/0. */
@@ -168,7 +184,8 @@ int sdk_set_solve_kernel(int kernel);
  * before a wave refills; tail: active lanes at or below which a drained wave
  * hands its last boards to the tail solver (0 off, at most 40); tail_mode: 1
  * the wave-wide solver continues each search, 0 the wave-per-board solver
- * restarts it; chunk: most boards a wave claims from the queue at once.  A
+ * restarts it; chunk: most boards a wave claims from the queue at once (at
+ * most 64: a claim is staged and converted in one go; 0 one claim per refill).  A
  * negative value keeps that knob; all four negative restore the defaults
  * ($SDK_PLANE_REFILL / _TAIL / _TAIL_MODE / _CHUNK).  Results never depend on
  * them.  Returns 0, or -1 for an out-of-range value (nothing changed). */

@@ -3,7 +3,8 @@ profiles/pmc_<kernel>.json (read by bench.py for the VALU roofline).
 
     python scripts/pmc_summarize.py OUT.json BATCH SEED DIR [DIR ...]
 
-Each DIR holds one pass's *counter_collection.csv.  Only solve_kernel
+Each DIR holds one pass's *counter_collection.csv (and DIR.log the profiled
+bench's output, whose JSON line gives the launch shape).  Only solve_kernel
 dispatches of the full batch are used (largest grid); values are averaged
 per dispatch.  FETCH_SIZE is doubled per MI355X_MICROARCH.md §HBM (gfx950
 reports half of a coalesced stream's bytes); sizes are in KB.
@@ -42,7 +43,18 @@ def main():
         for (disp, name), v in per.items():
             vals[name].append(v)
     summary = {k: sum(v) / len(v) for k, v in vals.items()}
-    res = {"kernel": kernel or "plane_kernel", "batch": batch, "seed": seed,
+    # the launch shape the profiled bench ran (its own JSON line, in each
+    # pass's log): bench.py uses these counters only for that exact shape
+    shape = None
+    for d in dirs:
+        try:
+            with open(d + ".log") as fh:
+                for ln in fh:
+                    if ln.startswith('{"metric"'):
+                        shape = shape or json.loads(ln)["roofline"]["shape"]
+        except OSError:
+            pass
+    res = {"kernel": kernel or "plane_kernel", "batch": batch, "seed": seed, "shape": shape,
            "workload": os.environ.get("PMC_WORKLOAD", "hard17"),
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),

@@ -28,6 +28,7 @@ EXPORTS = (
     "sdk_workspace_bytes",
     "sdk_solve_batch",
     "sdk_solve_batch_grid",
+    "sdk_solve_batches",
     "sdk_check_batch",
     "sdk_first_candidate_batch",
     "sdk_peer_solve_batch",
@@ -42,6 +43,7 @@ EXPORTS = (
     "sdk_set_plane_tuning",
 )
 SDK_KERNELS = {"auto": 1, "packed": 5, "plane": 6}
+SDK_MAX_BATCHES = 16  # sdk_solve_batches: batches per launch
 # device symbol of each solve kernel (rocprofv3 Kernel_Name, profiles/pmc_<symbol>.json)
 KERNEL_SYMBOLS = {1: "plane_kernel", 5: "solvep_kernel", 6: "plane_kernel"}
 
@@ -69,6 +71,9 @@ def load() -> ctypes.CDLL:
     L.sdk_solve_batch.argtypes = [vp, vp, vp, i64, vp, i32, i32, vp]
     L.sdk_solve_batch_grid.restype = i32
     L.sdk_solve_batch_grid.argtypes = [vp, vp, vp, i64, vp, i32, i32, vp, i32]
+    pp = ctypes.POINTER(ctypes.c_void_p)
+    L.sdk_solve_batches.restype = i32
+    L.sdk_solve_batches.argtypes = [pp, pp, pp, ctypes.POINTER(ctypes.c_int64), i32, vp, i32, vp, i32]
     L.sdk_check_batch.restype = i32
     L.sdk_check_batch.argtypes = [vp, vp, i64, i32, vp]
     L.sdk_first_candidate_batch.restype = i32

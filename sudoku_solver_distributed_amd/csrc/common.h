@@ -72,10 +72,27 @@ __device__ __forceinline__ int order_cell(uint64_t eb0, uint64_t eb1, int order)
     return m ? __builtin_ctzll(m) : 64 + __builtin_ctzll(eb1);
 }
 
+// Several batches in one plane launch (sdk_solve_batches): the queue hands
+// out virtual indices over the batches laid end to end; a lane's board id is
+// batch j << PLANE_BATCH_SHIFT | index in batch j (deferred-list entries too).
+// Passed by value as a kernel argument (520 bytes).
+struct PlaneBatches {
+    int64_t end[SDK_MAX_BATCHES];  // virtual index one past batch j (cumulative, ascending)
+    const uint8_t *in[SDK_MAX_BATCHES];
+    uint8_t *out[SDK_MAX_BATCHES];
+    int32_t *status[SDK_MAX_BATCHES];
+    int count;
+};
+#define PLANE_BATCH_SHIFT 40
+#define PLANE_LOCAL_MASK ((1ll << PLANE_BATCH_SHIFT) - 1)
+
 // Launch the plane kernel (plane_kernels.hip) and report its occupancy.
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
                             unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
                             int64_t threads, hipStream_t st);
+// the same over several batches (unordered only)
+hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws, uint32_t *stack,
+                                  int64_t *defer_list, int order, int64_t threads, hipStream_t st);
 int sdk_plane_blocks_per_cu();
 #define PLANE_MAX_DEPTH 32
 // plane kernel workgroup: ONE wave.  Its waves share nothing (each has its

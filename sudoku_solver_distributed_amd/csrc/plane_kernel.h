@@ -212,24 +212,93 @@ __device__ __forceinline__ bool plane_givens_clash(const uint8_t *__restrict__ s
     return plane::givens_clash(G, given);
 }
 
-// Hand board p to the wave kernel (status SDK_DEFERRED + an entry in the
-// deferred list; past PLANE_DEFER_CAP entries the wave kernel scans statuses).
-__device__ __forceinline__ void plane_defer(int64_t p, int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+// Hand board p (status word st) to the wave kernel (status SDK_DEFERRED + an
+// entry in the deferred list; past PLANE_DEFER_CAP entries the wave kernel
+// scans statuses).
+__device__ __forceinline__ void plane_defer(int32_t *st, int64_t p, unsigned long long *__restrict__ ws,
                                             int64_t *__restrict__ list)
 {
-    status[p] = SDK_DEFERRED;
+    *st = SDK_DEFERRED;
     const unsigned long long k = atomicAdd(&ws[WS_DEFER_COUNT], 1ull);
     if (k < (unsigned long long)PLANE_DEFER_CAP) list[k] = p;
     else atomicOr(&ws[WS_DEFER_OVER], 1ull);
 }
 
+// ---- board I/O of one launch.  The queue hands out VIRTUAL indices v over
+// the launch's boards; a claimed range is staged one batch segment at a time
+// (seg_*), and a lane keeps its board's id p (src / dst / stat).  One batch
+// (PlaneIO1, sdk_solve_batch): p = v = the board's index.  Several batches
+// (PlaneIOn, sdk_solve_batches): p = j << PLANE_BATCH_SHIFT | index in batch
+// j, and v runs over the batches laid end to end.
+struct PlaneIO1 {
+    static constexpr bool multi = false;
+    const uint8_t *in;
+    uint8_t *out;
+    int32_t *st;
+    int64_t n;
+    __device__ __forceinline__ int64_t total() const { return n; }
+    __device__ __forceinline__ const uint8_t *src(int64_t p) const { return in + p * 81; }
+    __device__ __forceinline__ uint8_t *dst(int64_t p) const { return out + p * 81; }
+    __device__ __forceinline__ int32_t *stat(int64_t p) const { return st + p; }
+    // board p's batch, as (input, output, status, index) for the wave solver
+    __device__ __forceinline__ const uint8_t *b_in(int64_t) const { return in; }
+    __device__ __forceinline__ uint8_t *b_out(int64_t) const { return out; }
+    __device__ __forceinline__ int32_t *b_st(int64_t) const { return st; }
+    __device__ __forceinline__ int64_t local(int64_t p) const { return p; }
+    // the segment from virtual v: its end (at most hi), v's id, the batch's
+    // input, its size and v's index in it
+    __device__ __forceinline__ int64_t seg_end(int64_t, int64_t hi) const { return hi; }
+    __device__ __forceinline__ int64_t id(int64_t v) const { return v; }
+    __device__ __forceinline__ const uint8_t *seg_in(int64_t) const { return in; }
+    __device__ __forceinline__ int64_t seg_n(int64_t) const { return n; }
+    __device__ __forceinline__ int64_t seg_local(int64_t v) const { return v; }
+};
+
+struct PlaneIOn {
+    static constexpr bool multi = true;
+    const PlaneBatches &b;
+    __device__ __forceinline__ int64_t total() const { return b.end[b.count - 1]; }
+    // batch of virtual v (wave-uniform: a scalar loop over at most 15 bounds)
+    __device__ __forceinline__ int batch(int64_t v) const
+    {
+        int j = 0;
+        for (int k = 0; k + 1 < b.count; ++k) j += v >= b.end[k];
+        return j;
+    }
+    __device__ __forceinline__ int64_t start(int j) const { return j ? b.end[j - 1] : 0; }
+    __device__ __forceinline__ const uint8_t *b_in(int64_t p) const { return b.in[p >> PLANE_BATCH_SHIFT]; }
+    __device__ __forceinline__ uint8_t *b_out(int64_t p) const { return b.out[p >> PLANE_BATCH_SHIFT]; }
+    __device__ __forceinline__ int32_t *b_st(int64_t p) const { return b.status[p >> PLANE_BATCH_SHIFT]; }
+    __device__ __forceinline__ int64_t local(int64_t p) const { return p & PLANE_LOCAL_MASK; }
+    __device__ __forceinline__ const uint8_t *src(int64_t p) const { return b_in(p) + local(p) * 81; }
+    __device__ __forceinline__ uint8_t *dst(int64_t p) const { return b_out(p) + local(p) * 81; }
+    __device__ __forceinline__ int32_t *stat(int64_t p) const { return b_st(p) + local(p); }
+    __device__ __forceinline__ int64_t seg_end(int64_t v, int64_t hi) const
+    {
+        const int64_t e = b.end[batch(v)];
+        return e < hi ? e : hi;
+    }
+    __device__ __forceinline__ int64_t id(int64_t v) const
+    {
+        const int j = batch(v);
+        return ((int64_t)j << PLANE_BATCH_SHIFT) | (v - start(j));
+    }
+    __device__ __forceinline__ const uint8_t *seg_in(int64_t v) const { return b.in[batch(v)]; }
+    __device__ __forceinline__ int64_t seg_n(int64_t v) const
+    {
+        const int j = batch(v);
+        return b.end[j] - start(j);
+    }
+    __device__ __forceinline__ int64_t seg_local(int64_t v) const { return v - start(batch(v)); }
+};
+
 // A drained wave's last boards (lanes `act`, board index p_lo / p_hi per
 // lane), each restarted on the whole wave by the wave-per-board solver.  Runs
 // after the pass loop, so the planes' registers are free for it.
 // st: solved, guesses, sweeps (wave-uniform).
+template <class IO>
 __device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, uint32_t p_lo, uint32_t p_hi,
-                                        const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols,
-                                        int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+                                        const IO &io, unsigned long long *__restrict__ ws,
                                         const int64_t *best, int order, uint32_t (&st)[3])
 {
     PCells cs;
@@ -239,7 +308,8 @@ __device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, u
         const int i = __builtin_ctzll(act);
         act &= act - 1;
         const int64_t pi = ((int64_t)rdlane(p_hi, i) << 32) | rdlane(p_lo, i);
-        psolve_board(W, lane, cs, puzzles, sols, status, pi, ws, best, order, solved, guesses, sweeps);
+        psolve_board(W, lane, cs, io.b_in(pi), io.b_out(pi), io.b_st(pi), io.local(pi), ws, best, order, solved,
+                     guesses, sweeps);
     }
     st[0] = solved;
     st[1] = guesses;
@@ -321,7 +391,7 @@ __device__ __forceinline__ void plane_stage_words(const uint32_t *stage, uint32_
 // 64 lanes writing / reading one word each hit 64 different banks).  A
 // refill then hands record i to the idle lane of rank i: every loaded lane
 // reads its own record at once, no per-board serial work.
-enum { PLANE_REC = 13 };
+enum { PLANE_REC = 13, PLANE_CHUNK_MAX = 64 };
 static_assert(64 * PLANE_REC + 1 < PLANE_STAGE_DWORDS, "chunk records");
 
 __device__ __forceinline__ void plane_convert_chunk(uint32_t *stage, uint32_t sh, int count, int lane)
@@ -362,15 +432,15 @@ __device__ __forceinline__ uint32_t plane_unguard(uint32_t v)
 // byte otherwise (they hold neighbouring boards' bytes).  Byte expansion:
 // value bit k of 4 consecutive cells, a nibble of the slice's 81-bit cell
 // stream, spreads to bit k of 4 bytes with one multiply (bit i -> bit 8i).
-__device__ __forceinline__ void plane_flush_outbox(const uint32_t *outbox, uint32_t count, int lane,
-                                                   uint8_t *__restrict__ sols)
+template <class IO>
+__device__ __forceinline__ void plane_flush_outbox(const uint32_t *outbox, uint32_t count, int lane, const IO &io)
 {
     if ((uint32_t)lane < count) {
         const sdk_v4u *rec = (const sdk_v4u *)(outbox + PLANE_OB_WORDS * lane);
         const sdk_v4u r0 = rec[0], r1 = rec[1], r2 = rec[2], r3 = rec[3];
         const uint32_t V[4][3] = {{r0.x, r0.y, r0.z}, {r0.w, r1.x, r1.y}, {r1.z, r1.w, r2.x}, {r2.y, r2.z, r2.w}};
         const int64_t pb = ((int64_t)r3.y << 32) | r3.x;
-        uint8_t *dst = sols + pb * 81;
+        uint8_t *dst = io.dst(pb);
         const uint32_t sh = (uint32_t)(uintptr_t)dst & 3u;
         uint32_t *dw = (uint32_t *)(dst - sh);
         // per slice: the 81-bit cell stream, shifted up by sh bits (byte
@@ -457,9 +527,9 @@ struct WideStack {
 // Solve the k boards recorded in `recs` on the wave-wide solver, one after
 // the other.  st: solved, guesses (net of deferred boards'), passes,
 // deferred -- wave-uniform.
+template <class IO>
 __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
-                                             const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols,
-                                             int32_t *__restrict__ status, unsigned long long *__restrict__ ws,
+                                             const IO &io, unsigned long long *__restrict__ ws,
                                              int64_t *__restrict__ defer_list, const int64_t *best, int node_order,
                                              uint32_t (&st)[5])
 {
@@ -482,8 +552,8 @@ __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int
         });
         passes += ws_.passes;
         guesses += ws_.guesses;
-        const uint8_t *src = puzzles + pb * 81;
-        uint8_t *dst = sols + pb * 81;
+        const uint8_t *src = io.src(pb);
+        uint8_t *dst = io.dst(pb);
         if (r == wide::W_SOLVED) {
             uint32_t sl[4];
             wide::value_slices(w, L, sl);
@@ -496,22 +566,22 @@ __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int
             if (c0 >= 0) dst[c0] = (uint8_t)v0;
             if (c1 >= 0) dst[c1] = (uint8_t)v1;
             if (lane == 0) {
-                status[pb] = SDK_SOLVED;
+                *io.stat(pb) = SDK_SOLVED;
                 if (best) __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], pb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             }
             solved++;
         } else if (r == wide::W_CANCELLED) {
             plane_copy_board(src, dst, lane);
-            if (lane == 0) status[pb] = SDK_CANCELLED;
+            if (lane == 0) *io.stat(pb) = SDK_CANCELLED;
         } else if (r == wide::W_OVERFLOW || plane_givens_clash(src, c0, c1)) {
             // too deep for the stack, or no completion on clashing givens
             // (rules B/C unsound): the wave kernel's
-            if (lane == 0) plane_defer(pb, status, ws, defer_list);
+            if (lane == 0) plane_defer(io.stat(pb), pb, ws, defer_list);
             deferred++;
             guesses -= ws_.bguess;
         } else {
             plane_copy_board(src, dst, lane);
-            if (lane == 0) status[pb] = SDK_UNSOLVABLE;
+            if (lane == 0) *io.stat(pb) = SDK_UNSOLVABLE;
         }
     }
     st[0] = solved;
@@ -539,11 +609,14 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 #ifndef SDK_PLANE_WAVES_PER_EU
 #define SDK_PLANE_WAVES_PER_EU 4
 #endif
-__global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
-    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
-    unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int tail_mode, int chunk)
+// The kernel body over either board I/O (plane_kernel: one batch;
+// plane_kernel_multi: several, unordered).
+template <class IO>
+__device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__restrict__ ws,
+                                           uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list,
+                                           int ordered, int order, int refill, int tail, int tail_mode, int chunk)
 {
+    const int64_t n = io.total();  // boards of the launch (virtual indices 0..n-1)
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     __shared__ __attribute__((aligned(16))) uint32_t outbox_lds[PLANE_THREADS / 64][PLANE_OUTBOX * PLANE_OB_WORDS];
@@ -579,7 +652,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     // refill (the head is one device-scope atomic for 4096 waves).  Chunks
     // shrink towards the end of the batch (guided: remaining / (2 waves)).
     int64_t res_lo = 0, res_hi = 0;
-    int64_t rec_base = 0;  // board of chunk record 0 (SDK_PLANE_PRECONV)
+    int64_t rec_base = 0;  // virtual index of chunk record 0 (SDK_PLANE_PRECONV)
+    int64_t rec_id = 0;    // its board id
+    int64_t seg_hi = 0;    // [res_lo, seg_hi) converted (one batch segment), [seg_hi, res_hi) claimed only
     bool queue_out = false;
     const int64_t nwaves = (int64_t)gridDim.x * (PLANE_THREADS / 64);
     uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
@@ -597,16 +672,16 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
 
     // Start-up: the wave's first 64 boards arrive as one staged span; each
     // lane then converts its own board (plane::load_words), all lanes at once.
-    {
+    if constexpr (!IO::multi) {
         const unsigned long long base = (unsigned long long)(g - lane);
         queue_out = nt >= n;
         drained = queue_out;
         const int64_t q = (int64_t)base + lane;
         const int64_t kk = (int64_t)base < n ? (n - (int64_t)base < 64 ? n - (int64_t)base : 64) : 0;
-        const uint32_t sh = kk ? plane_stage_span(puzzles, n, (int64_t)base, (int)kk, stage, lane) : 0u;
+        const uint32_t sh = kk ? plane_stage_span(io.in, n, (int64_t)base, (int)kk, stage, lane) : 0u;
         if (q < n) {
             fin++;
-            const uint8_t *src = puzzles + q * 81;
+            const uint8_t *src = io.src(q);
             uint32_t x[21];
             plane_stage_words(stage, sh + 81u * (uint32_t)lane, x);
             bool clash;  // tested lazily (see the unsolvable store above)
@@ -618,9 +693,42 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 bguess = 0;
                 state = PL_ACTIVE;
             } else {
-                for (int i = 0; i < 81; ++i) sols[q * 81 + i] = src[i];  // raw input back
-                status[q] = ok ? SDK_CANCELLED : SDK_INVALID;
+                for (int i = 0; i < 81; ++i) io.out[q * 81 + i] = src[i];  // raw input back
+                *io.stat(q) = ok ? SDK_CANCELLED : SDK_INVALID;
             }
+        }
+    } else {
+        const int64_t v0 = g - lane;
+        queue_out = nt >= n;
+        drained = queue_out;
+        const int64_t kk = v0 < n ? (n - v0 < 64 ? n - v0 : 64) : 0;
+        // one staged span per batch segment of the window (one for one batch)
+        for (int64_t s0 = 0; s0 < kk;) {
+            const int64_t sv = v0 + s0, se = io.seg_end(sv, v0 + kk);
+            const int cnt = (int)(se - sv);
+            const uint32_t sh = plane_stage_span(io.seg_in(sv), io.seg_n(sv), io.seg_local(sv), cnt, stage, lane);
+            const int r = lane - (int)s0;
+            if (r >= 0 && r < cnt) {
+                const int64_t q = io.id(sv) + r;
+                fin++;
+                uint32_t x[21];
+                plane_stage_words(stage, sh + 81u * (uint32_t)r, x);
+                bool clash;  // tested lazily (see the unsolvable store above)
+                const bool ok = plane::load_words(B, x, clash);
+                const bool cancel = ok && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q;
+                if (ok && !cancel) {
+                    p = q;
+                    depth = 0;
+                    bguess = 0;
+                    state = PL_ACTIVE;
+                } else {
+                    const uint8_t *src = io.src(q);
+                    uint8_t *dst = io.dst(q);
+                    for (int i = 0; i < 81; ++i) dst[i] = src[i];  // raw input back
+                    *io.stat(q) = ok ? SDK_CANCELLED : SDK_INVALID;
+                }
+            }
+            s0 = se - v0;
         }
     }
 
@@ -651,7 +759,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             if (m) {
                 const uint32_t ns = (uint32_t)__builtin_popcountll(m);
                 if (ob_count + ns > (uint32_t)PLANE_OUTBOX) {
-                    plane_flush_outbox(outbox, ob_count, lane, sols);
+                    plane_flush_outbox(outbox, ob_count, lane, io);
                     ob_count = 0;
                 }
                 if (state == PL_SOLVED) {
@@ -668,7 +776,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     rec[1] = (sdk_v4u){V[1][1], V[1][2], V[2][0], V[2][1]};
                     rec[2] = (sdk_v4u){V[2][2], V[3][0], V[3][1], V[3][2]};
                     rec[3] = (sdk_v4u){(uint32_t)p, (uint32_t)(p >> 32), 0u, 0u};
-                    status[p] = SDK_SOLVED;  // every solved lane its own, one store
+                    *io.stat(p) = SDK_SOLVED;  // every solved lane its own, one store
                 }
                 ob_count += ns;
             }
@@ -679,21 +787,21 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 m &= m - 1;
                 const int64_t pi = ((int64_t)rdlane((uint32_t)(p >> 32), i) << 32) | rdlane((uint32_t)p, i);
                 const bool cancelled = rdlane((uint32_t)state, i) == PL_CANCELLED;
-                if (!cancelled && plane_givens_clash(puzzles + pi * 81, c0, c1)) {
+                if (!cancelled && plane_givens_clash(io.src(pi), c0, c1)) {
                     // rules B/C are unsound on givens that repeat a digit in a
                     // unit: "no completion" is the packed kernel's call.  (A
                     // SOLVED result needs every unit to hold every digit, so
                     // such givens never reach the store above.)
                     if (lane == i) {
-                        plane_defer(pi, status, ws, defer_list);
+                        plane_defer(io.stat(pi), pi, ws, defer_list);
                         fin--;
                         deferred++;
                         guesses -= bguess;
                     }
                     continue;
                 }
-                plane_copy_board(puzzles + pi * 81, sols + pi * 81, lane);
-                if (lane == 0) status[pi] = cancelled ? SDK_CANCELLED : SDK_UNSOLVABLE;
+                plane_copy_board(io.src(pi), io.dst(pi), lane);
+                if (lane == 0) *io.stat(pi) = cancelled ? SDK_CANCELLED : SDK_UNSOLVABLE;
             }
             if (state != PL_ACTIVE) state = PL_IDLE;
             // ---- refill the free lanes: one queue add per wave; the boards'
@@ -723,6 +831,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     // a conversion, and all waves then drain at once
                     int64_t c = chunk > 0 ? (n - (res_hi > nt ? res_hi : nt)) / (2 * nwaves) : 0;
                     c = c > chunk ? chunk : c;
+                    // a chunk is staged and converted in one go: at most 64 records
+                    // fit the staging area (the host also rejects chunk > 64)
+                    c = c > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : c;
                     c = c < k ? k : c;
                     if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)c);
 #if SDK_PLANE_STAMPS
@@ -734,18 +845,37 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     if (res_lo > n) res_lo = n;
                     queue_out = res_lo + c >= n;
 #if SDK_PLANE_PRECONV
-                    // the whole chunk staged and converted once (chunk records)
-                    const int cc = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo));
-                    rec_base = res_lo;
-                    if (cc) {
-                        const uint32_t sh = plane_stage_span(puzzles, n, res_lo, cc, stage, lane);
-                        plane_convert_chunk(stage, sh, cc, lane);
+                    if constexpr (!IO::multi) {
+                        // the whole chunk staged and converted once (chunk records)
+                        const int cc = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo));
+                        rec_base = res_lo;
+                        if (cc) {
+                            const uint32_t sh = plane_stage_span(io.in, n, res_lo, cc, stage, lane);
+                            plane_convert_chunk(stage, sh, cc, lane);
+                        }
                     }
+                    seg_hi = IO::multi ? res_lo : res_hi;  // (multi: nothing converted yet)
+#else
+                    seg_hi = res_hi;
 #endif
                 }
+#if SDK_PLANE_PRECONV
+                if (IO::multi && res_lo == seg_hi && res_lo < res_hi) {
+                    // the claimed chunk staged and converted once (chunk
+                    // records), a batch segment at a time (one for one batch)
+                    seg_hi = io.seg_end(res_lo, res_hi);
+                    const int cc = __builtin_amdgcn_readfirstlane((int)(seg_hi - res_lo));
+                    rec_base = res_lo;
+                    rec_id = io.id(res_lo);
+                    const uint32_t sh = plane_stage_span(io.seg_in(res_lo), io.seg_n(res_lo), io.seg_local(res_lo), cc,
+                                                         stage, lane);
+                    plane_convert_chunk(stage, sh, cc, lane);
+                }
+#endif
                 base = (unsigned long long)res_lo;
                 // (wave-uniform: readfirstlane keeps the deposit loop a scalar loop)
-                const int kk = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo < k ? res_hi - res_lo : k));
+                const int64_t avail = (IO::multi ? seg_hi : res_hi) - res_lo;
+                const int kk = __builtin_amdgcn_readfirstlane((int)(avail < k ? avail : k));
                 res_lo += kk;
                 drained = queue_out && res_lo == res_hi;
 #if SDK_PLANE_STAMPS
@@ -771,7 +901,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                             for (int b = 0; b < 3; ++b) V[s][b] = rec[3 * s + b];
                         bad = rec[12] != 0u;
                         fin++;
-                        p = (int64_t)base + (int64_t)rank;
+                        p = (IO::multi ? rec_id + ((int64_t)base - rec_base) : (int64_t)base) + (int64_t)rank;
                         depth = 0;
                         bguess = 0;
                         if (!bad && !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
@@ -787,9 +917,10 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     while (r) {
                         const int i = __builtin_ctzll(r);
                         r &= r - 1;
-                        const int64_t q = (int64_t)base + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
-                        plane_copy_board(puzzles + q * 81, sols + q * 81, lane);
-                        if (lane == 0) status[q] = ((badm >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
+                        const int64_t q = (IO::multi ? rec_id + ((int64_t)base - rec_base) : (int64_t)base) +
+                                          (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
+                        plane_copy_board(io.src(q), io.dst(q), lane);
+                        if (lane == 0) *io.stat(q) = ((badm >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
                     }
                     if (state == PL_CANCELLED) state = PL_IDLE;
 #if SDK_PLANE_STAMPS
@@ -798,7 +929,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 }
 #else
                 if (kk) {
-                    const uint32_t sh = plane_stage_span(puzzles, n, (int64_t)base, kk, stage, lane);
+                    const uint32_t sh = plane_stage_span(io.seg_in((int64_t)base), io.seg_n((int64_t)base),
+                                                         io.seg_local((int64_t)base), kk, stage, lane);
 #if SDK_PLANE_STAMPS
                     const uint64_t st_r2 = __builtin_amdgcn_s_memtime();
                     st_dma += st_r2 - st_r1;
@@ -841,7 +973,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     }
                     if ((loaded >> lane) & 1u) {
                         fin++;
-                        p = (int64_t)base + (int64_t)lanes_below(loaded);
+                        p = io.id((int64_t)base) + (int64_t)lanes_below(loaded);
                         depth = 0;
                         bguess = 0;
                         if (!((bad >> lane) & 1u) &&
@@ -862,9 +994,9 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                     while (r) {
                         const int i = __builtin_ctzll(r);
                         r &= r - 1;
-                        const int64_t q = (int64_t)base + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
-                        plane_copy_board(puzzles + q * 81, sols + q * 81, lane);
-                        if (lane == 0) status[q] = ((bad >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
+                        const int64_t q = io.id((int64_t)base) + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
+                        plane_copy_board(io.src(q), io.dst(q), lane);
+                        if (lane == 0) *io.stat(q) = ((bad >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
                     }
                     if (state == PL_CANCELLED) state = PL_IDLE;
 #if SDK_PLANE_STAMPS
@@ -906,7 +1038,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
                 __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else if (r == plane::STUCK) {
             if (depth == PLANE_MAX_DEPTH) {
-                plane_defer(p, status, ws, defer_list);  // too deep for the stack: the wave kernel's
+                plane_defer(io.stat(p), p, ws, defer_list);  // too deep for the stack: the wave kernel's
                 fin--;
                 deferred++;
                 guesses -= bguess;
@@ -956,7 +1088,7 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
             }
         }
     }
-    if (ob_count) plane_flush_outbox(outbox, ob_count, lane, sols);
+    if (ob_count) plane_flush_outbox(outbox, ob_count, lane, io);
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
     const uint64_t st_t3 = __builtin_amdgcn_s_memrealtime();  // the lane loop ended
@@ -981,8 +1113,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         }
         wave_lds_sync();
         uint32_t wst[5];
-        plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, puzzles, sols, status, ws, defer_list,
-                        best, node_order, wst);
+        plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, io, ws, defer_list, best, node_order,
+                        wst);
 #if SDK_PLANE_STAMPS
         st_tailp = wst[2];
 #endif
@@ -996,8 +1128,8 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
     } else if (tail_act) {
         // after the loop: the planes are dead, the wave solver gets the registers
         uint32_t wst[3];
-        plane_tail(tail_lds[threadIdx.x >> 6], lane, tail_act, (uint32_t)p, (uint32_t)(p >> 32), puzzles, sols,
-                   status, ws, best, order, wst);
+        plane_tail(tail_lds[threadIdx.x >> 6], lane, tail_act, (uint32_t)p, (uint32_t)(p >> 32), io, ws, best, order,
+                   wst);
         if (lane == 0) {
             solved += wst[0];
             guesses += wst[1];
@@ -1040,6 +1172,24 @@ __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_k
         atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
         atomicAdd(&ws[WS_SWEEPS], (unsigned long long)passes);
     }
+}
+
+__global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
+    const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
+    unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
+    int order, int refill, int tail, int tail_mode, int chunk)
+{
+    const PlaneIO1 io = {puzzles, sols, status, n};
+    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk);
+}
+
+// several batches, one queue over them (sdk_solve_batches; unordered)
+__global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel_multi(
+    const PlaneBatches bs, unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack,
+    int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk)
+{
+    const PlaneIOn io = {bs};
+    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk);
 }
 
 #endif  // SDK_PLANE_KERNEL_H

@@ -29,7 +29,7 @@ static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1};
 
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 {
-    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 1 || refill == 0) return -1;
+    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 1 || refill == 0 || chunk > PLANE_CHUNK_MAX) return -1;
     if (refill < 0 && tail < 0 && tail_mode < 0 && chunk < 0) {
         g_refill = g_tail = g_tail_mode = g_chunk = -1;
         return 0;
@@ -41,9 +41,11 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
     return 0;
 }
 
-hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
-                            unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
-                            int64_t threads, hipStream_t st)
+struct PlaneKnobs {
+    int refill, tail, tail_mode, chunk;
+};
+
+static PlaneKnobs plane_knobs()
 {
     static const int refill_env = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
     static const int tail_env = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
@@ -53,10 +55,29 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
     int tail = g_tail >= 0 ? g_tail.load() : tail_env;
     tail = tail > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail;
     const int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : tail_mode_env;
-    const int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
+    int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
+    chunk = chunk > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : chunk;  // ($SDK_PLANE_CHUNK is not range-checked)
+    return {refill, tail, tail_mode, chunk};
+}
+
+hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
+                            unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
+                            int64_t threads, hipStream_t st)
+{
+    const PlaneKnobs k = plane_knobs();
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, defer_list, ordered, order, refill, tail, tail_mode, chunk);
+                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk);
+    return hipGetLastError();
+}
+
+hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws, uint32_t *stack,
+                                  int64_t *defer_list, int order, int64_t threads, hipStream_t st)
+{
+    const PlaneKnobs k = plane_knobs();
+    const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
+    hipLaunchKernelGGL(plane_kernel_multi, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, bs, ws, stack,
+                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk);
     return hipGetLastError();
 }
 

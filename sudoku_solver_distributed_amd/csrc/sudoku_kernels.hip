@@ -130,6 +130,50 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
     pflush_stats(lane, ws, fin, solved, guesses, sweeps);
 }
 
+// The same for a plane_kernel_multi launch: list entries are board ids
+// (batch j << PLANE_BATCH_SHIFT | index), the overflow scan runs batch by batch.
+__global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep_deferred_multi_kernel(
+    const PlaneBatches bs, unsigned long long *__restrict__ ws, const int64_t *__restrict__ list, int order)
+{
+    __shared__ PackLds lds[WAVES_PER_BLOCK];
+    const int lane = threadIdx.x & 63;
+    PackLds &W = lds[threadIdx.x >> 6];
+    const int64_t nwaves = (int64_t)gridDim.x * WAVES_PER_BLOCK;
+    const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
+    const int64_t cnt = (int64_t)ws[WS_DEFER_COUNT];
+    const bool over = ws[WS_DEFER_OVER] != 0;
+    if (cnt == 0 || (!over && gw >= cnt)) return;
+
+    PCells s;
+    pinit_lane(s, lane);
+    uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
+    if (!over) {
+        for (int64_t k = gw; k < cnt; k += nwaves) {
+            const int64_t p = list[k];
+            const int j = (int)(p >> PLANE_BATCH_SHIFT);
+            psolve_board(W, lane, s, bs.in[j], bs.out[j], bs.status[j], p & PLANE_LOCAL_MASK, ws, nullptr, order,
+                         solved, guesses, sweeps);
+            fin++;
+        }
+    } else {
+        for (int j = 0; j < bs.count; ++j) {
+            const int64_t n = bs.end[j] - (j ? bs.end[j - 1] : 0);
+            for (int64_t base = gw * 64; base < n; base += nwaves * 64) {
+                const int32_t sv = base + lane < n ? bs.status[j][base + lane] : 0;
+                uint64_t m = __builtin_amdgcn_ballot_w64(sv == SDK_DEFERRED);
+                while (m) {
+                    const int i = __builtin_ctzll(m);
+                    m &= m - 1;
+                    psolve_board(W, lane, s, bs.in[j], bs.out[j], bs.status[j], base + i, ws, nullptr, order, solved,
+                                 guesses, sweeps);
+                    fin++;
+                }
+            }
+        }
+    }
+    pflush_stats(lane, ws, fin, solved, guesses, sweeps);
+}
+
 // ------------------------------------------------------------ check kernel
 // One thread per grid; the block stages its 64 grids (5184 B) through LDS
 // with coalesced dword loads.
@@ -583,6 +627,63 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
     }
     e = hipGetLastError();
     if (e != hipSuccess) return set_err("sdk_solve_batch: launch", e);
+    return 0;
+}
+
+int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutions, int32_t *const *d_status,
+                      const int64_t *n, int count, void *d_workspace, int order, void *stream, int grid_waves)
+{
+    if (count < 1 || count > SDK_MAX_BATCHES || !d_puzzles || !d_solutions || !d_status || !n || !d_workspace ||
+        (order != SDK_ORDER_GEN && order != SDK_ORDER_NODE) || grid_waves < 0) {
+        snprintf(g_err, sizeof g_err, "sdk_solve_batches: bad arguments (count=%d)", count);
+        return -2;
+    }
+    PlaneBatches bs = {};
+    int64_t total = 0;
+    for (int i = 0; i < count; ++i) {
+        if (n[i] < 0 || n[i] > PLANE_LOCAL_MASK || (n[i] > 0 && (!d_puzzles[i] || !d_solutions[i] || !d_status[i]))) {
+            snprintf(g_err, sizeof g_err, "sdk_solve_batches: bad batch %d (n=%lld)", i, (long long)n[i]);
+            return -2;
+        }
+        if (n[i] == 0) continue;  // empty batches take no slot
+        bs.in[bs.count] = d_puzzles[i];
+        bs.out[bs.count] = d_solutions[i];
+        bs.status[bs.count] = d_status[i];
+        total += n[i];
+        bs.end[bs.count] = total;
+        bs.count++;
+    }
+    if (bs.count == 0) return 0;
+    int variant = solve_variant();
+    if (variant == SDK_KERNEL_AUTO) variant = total >= SDK_PLANE_MIN_BATCH ? SDK_KERNEL_PLANE : SDK_KERNEL_PACKED;
+    if (bs.count == 1 || variant == SDK_KERNEL_PACKED) {
+        // one batch, or the wave-per-board kernel: the batches one after the other
+        for (int i = 0; i < bs.count; ++i) {
+            const int rc = sdk_solve_batch_grid(bs.in[i], bs.out[i], bs.status[i], bs.end[i] - (i ? bs.end[i - 1] : 0),
+                                                d_workspace, order, 0, stream, grid_waves);
+            if (rc) return rc;
+        }
+        return 0;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long *ws = (unsigned long long *)d_workspace;
+    std::lock_guard<std::mutex> lk(g_launch_mu);
+    hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
+    const int64_t max_threads = plane_max_threads();
+    const int64_t grid_cap = (int64_t)cu_count() * 4 * grid_waves * 64;
+    const int64_t lane_cap = grid_waves > 0 && grid_cap < max_threads ? grid_cap : max_threads;
+    const int64_t threads = total < lane_cap ? total : lane_cap;
+    uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
+    int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
+    hipError_t e = sdk_launch_plane_multi(bs, ws, stack, list, order, threads, st);
+    if (e != hipSuccess) return set_err("sdk_solve_batches: plane launch", e);
+    const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_deferred_multi_kernel, g_bpc_packed) * WAVES_PER_BLOCK;
+    const int64_t groups = (total + 63) / 64;
+    const int64_t waves = groups < max_waves ? groups : max_waves;
+    hipLaunchKernelGGL(solvep_deferred_multi_kernel, dim3((unsigned)((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
+                       dim3(BLOCK_THREADS), 0, st, bs, ws, (const int64_t *)list, order);
+    e = hipGetLastError();
+    if (e != hipSuccess) return set_err("sdk_solve_batches: launch", e);
     return 0;
 }
 

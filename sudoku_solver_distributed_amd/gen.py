@@ -11,7 +11,8 @@
 * ``hard17_batch(n, seed)``    -- the benchmark's hard set: 17-clue boards with
   a unique solution, made by validity-preserving symmetries (digit relabeling,
   row/column permutations inside bands/stacks, band/stack permutations,
-  transposition) of seed boards certified unique.
+  transposition) of the 80 certified isomorphism classes in
+  data/hard17_classes.txt (scripts/make_hard17.py).
 * ``hard_search_batch(n, seed)`` -- the search-heavy set: the same symmetries
   applied to 256 minimal puzzles that need real search (data/).
 """
@@ -31,10 +32,10 @@ from .sudoku import Sudoku
 # 17-clue boards with exactly one solution (certified by
 # tests/test_oracle.py::test_seeds_unique with the oracle's counter); the last
 # one is the "brute-force resistant" board whose solution's first row is
-# 987654321 -- a worst case for the walk.  hard17_batch makes every benchmark
-# board from these six, so the set has six isomorphism classes; their
-# logical difficulty is mostly singles (0.5 guesses per board), which is why
-# bench.py also reports a search-heavy side set (hard_search_batch).
+# 987654321 -- a worst case for the walk.  Through round 3 hard17_batch made
+# every benchmark board from these six (six isomorphism classes); they now
+# seed the corpus search (scripts/make_hard17.py -> data/hard17_classes.txt),
+# and bench.py also reports a search-heavy side set (hard_search_batch).
 SEEDS_17 = (
     "000000010400000000020000000000050407008000300001090000300400200050100000000806000",
     "000000010400000000020000000000050604008000300001090000300400200050100000000807000",
@@ -156,15 +157,28 @@ def _symmetry_images(base: np.ndarray, n: int, seed: int) -> np.ndarray:
     return np.take_along_axis(relabel, b.reshape(n, 81).astype(np.int64), axis=1).astype(np.uint8)
 
 
-def hard17_batch(n: int, seed: int = 0, seeds=SEEDS_17, device=None) -> torch.Tensor:
-    """n 17-clue unique-solution boards (symmetry images of `seeds`), as a
-    (n, 81) uint8 tensor on `device` (host if device is None)."""
+_DATA = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data")
+
+
+def hard17_classes() -> List[str]:
+    """The hard 17-clue corpus: one board per isomorphism class (minlex
+    form), each certified 17 clues + one completion (data/hard17_classes.txt,
+    made by scripts/make_hard17.py from SEEDS_17 by clue exchanges)."""
+    with open(os.path.join(_DATA, "hard17_classes.txt")) as f:
+        return [ln.split()[0] for ln in f if ln.strip() and not ln.startswith("#")]
+
+
+def hard17_batch(n: int, seed: int = 0, seeds=None, device=None) -> torch.Tensor:
+    """n 17-clue unique-solution boards (symmetry images of `seeds`, default
+    the hard17_classes() corpus), as a (n, 81) uint8 tensor on `device`
+    (host if device is None)."""
+    seeds = hard17_classes() if seeds is None else seeds
     base = np.array([[int(c) for c in s] for s in seeds], dtype=np.uint8)
     t = torch.from_numpy(np.ascontiguousarray(_symmetry_images(base, n, seed)))
     return t.to(device) if device is not None else t
 
 
-_HARD_SEARCH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "data", "hard_search_seeds.txt")
+_HARD_SEARCH = os.path.join(_DATA, "hard_search_seeds.txt")
 
 
 def hard_search_seeds() -> List[str]:

@@ -155,8 +155,13 @@ class GpuSolverBackend:
         return res
 
     def new_peer_state(self):
-        """A new node's persistent /solve state (node.py:149, 167)."""
-        return self.solvers[0].new_peer_state()
+        """A new node's persistent /solve state (node.py:149, 167), zeroed on
+        the stream peer_solve_seq runs on (streams[0] is a non-blocking pool
+        stream: a memset on the caller's stream would not be ordered before
+        the first request)."""
+        s, stream = self.solvers[0], self.streams[0]
+        with torch.cuda.device(s.device), torch.cuda.stream(stream):
+            return s.new_peer_state()
 
     def peer_solve_seq(self, boards: torch.Tensor, state):
         """The reference's /solve loop on ONE node serving `boards` as

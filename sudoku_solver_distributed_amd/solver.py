@@ -90,6 +90,8 @@ class BatchSolver:
         # held by callers that need solve + stats as one step (node.py's backend)
         self.op_lock = threading.RLock()
         self._pool = None  # the solver's streams (_stream_pool)
+        self._slots = None  # solve_inflight's (solver, stream) slots (_slot_solvers)
+        self._pool_lock = threading.Lock()  # builds _pool / _slots once across threads
         with torch.cuda.device(self.device):
             self.workspace = torch.zeros(int(self.lib.sdk_workspace_bytes()), dtype=torch.uint8,
                                          device=self.device)
@@ -140,29 +142,58 @@ class BatchSolver:
         _lib.check(rc, "sdk_solve_batch_grid")
         return out, status
 
+    def solve_batches(self, batches, outs, statuses, order="gen", stream=None, grid_waves: int = 0):
+        """Several device batches solved by ONE launch sequence
+        (sdk_solve_batches): the lane-per-board kernel's queue runs over the
+        batches laid end to end and drains once, so batches too small to fill
+        the GPU on their own (a multi-GPU shard of one step) keep every lane
+        busy.  Each batch's outputs are exactly solve()'s.  At most
+        SDK_MAX_BATCHES (16) batches; unordered only."""
+        if not (len(batches) == len(outs) == len(statuses)) or not 1 <= len(batches) <= _lib.SDK_MAX_BATCHES:
+            raise ValueError(f"1..{_lib.SDK_MAX_BATCHES} batches, one out and one status tensor each")
+        ps = [self._dev(as_boards(b)) for b in batches]
+        for p, o, st in zip(ps, outs, statuses):
+            if o.shape != p.shape or o.dtype != torch.uint8 or not o.is_contiguous() or o.device != self.device:
+                raise ValueError("each out must be a contiguous (n, 81) uint8 tensor on the solver's device")
+            if st.shape != (p.shape[0],) or st.dtype != torch.int32 or st.device != self.device:
+                raise ValueError("each status must be an (n,) int32 tensor on the solver's device")
+        k = len(ps)
+        arr = ctypes.c_void_p * k
+        ins = arr(*[p.data_ptr() for p in ps])
+        out_p = arr(*[o.data_ptr() for o in outs])
+        st_p = arr(*[st.data_ptr() for st in statuses])
+        ns = (ctypes.c_int64 * k)(*[p.shape[0] for p in ps])
+        with self._lock, torch.cuda.device(self.device):
+            rc = self.lib.sdk_solve_batches(ins, out_p, st_p, ns, k, self.workspace.data_ptr(), _lib.order_code(order),
+                                            self._ws_stream(stream), int(grid_waves))
+        _lib.check(rc, "sdk_solve_batches")
+        return list(zip(outs, statuses))
+
     def _stream_pool(self, k: int):
         """The solver's own streams, created once and shared by solve_host
         (compute, copy-in) and solve_inflight (one per slot): a process has
         few hardware queues (4), and streams past them share a queue and
         serialise."""
-        if self._pool is None:
-            self._pool = []
-        while len(self._pool) < k:
-            self._pool.append(torch.cuda.Stream(self.device))
-        return self._pool[:k]
+        with self._pool_lock:
+            if self._pool is None:
+                self._pool = []
+            while len(self._pool) < k:
+                self._pool.append(torch.cuda.Stream(self.device))
+            return self._pool[:k]
 
     def _slot_solvers(self, inflight: int):
         """[self] + inflight - 1 more solvers on this device, each with its
         own workspace (~1.1 GB: per-lane stacks) and its own stream."""
         streams = self._stream_pool(inflight)
-        if not hasattr(self, "_slots"):
-            self._slots = [(self, streams[0])]
-        while len(self._slots) < inflight:
-            self._slots.append((BatchSolver(self.device), streams[len(self._slots)]))
-        return self._slots[:inflight]
+        with self._pool_lock:
+            if self._slots is None:
+                self._slots = [(self, streams[0])]
+            while len(self._slots) < inflight:
+                self._slots.append((BatchSolver(self.device), streams[len(self._slots)]))
+            return self._slots[:inflight]
 
     def solve_inflight(self, batches, outs, statuses, inflight: int = 3, order="gen", ordered: bool = False,
-                       launch_events=None, grid_waves: Optional[int] = None):
+                       launch_events=None, grid_waves: Optional[int] = None, group: int = 1):
         """Solve a sequence of device batches with up to `inflight` launches
         in flight on this GPU: batch i runs on slot i % inflight (its own
         workspace and stream), so a launch's end -- its last boards draining
@@ -174,29 +205,44 @@ class BatchSolver:
         batches that may be in flight together must not alias).  The
         caller's current stream waits for every batch; nothing synchronises
         the host.  launch_events: optional list that receives a (start, end)
-        timing-event pair per batch, recorded on its slot's stream."""
+        timing-event pair per launch, recorded on its slot's stream.
+        group > 1: each launch solves `group` consecutive batches at once
+        (solve_batches, one queue over them; unordered only) -- the
+        strong-scaling steps, where one GPU's share of a step is too small to
+        fill the GPU alone."""
         if inflight < 1:
             raise ValueError("inflight must be >= 1")
+        if not 1 <= group <= _lib.SDK_MAX_BATCHES or (group > 1 and ordered):
+            raise ValueError(f"group must be 1..{_lib.SDK_MAX_BATCHES} (and 1 in ordered mode)")
         if not (len(batches) == len(outs) == len(statuses)):
             raise ValueError("one out and one status tensor per batch")
         if grid_waves is None:
             grid_waves = GRID_WAVES_INFLIGHT if inflight > 1 else 0
         slots = self._slot_solvers(inflight)
         caller = torch.cuda.current_stream(self.device)
+        # every batch in its final form (contiguous uint8 on this device)
+        # BEFORE `ready` is recorded: a conversion enqueued on the caller
+        # stream after it would race the slot stream's kernel
+        batches = [self._dev(as_boards(b)) for b in batches]
         ready = torch.cuda.Event()
         ready.record(caller)
         for _, s in slots:
             s.wait_event(ready)
-        for i, (b, o, st) in enumerate(zip(batches, outs, statuses)):
+        for i, lo in enumerate(range(0, len(batches), group)):
             solver, s = slots[i % inflight]
+            bs, os_, sts = batches[lo:lo + group], outs[lo:lo + group], statuses[lo:lo + group]
             if launch_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
-            solver.solve(b, out=o, status=st, order=order, ordered=ordered, stream=s, grid_waves=grid_waves)
+            if group == 1:
+                solver.solve(bs[0], out=os_[0], status=sts[0], order=order, ordered=ordered, stream=s,
+                             grid_waves=grid_waves)
+            else:
+                solver.solve_batches(bs, os_, sts, order=order, stream=s, grid_waves=grid_waves)
             if launch_events is not None:
                 e1.record(s)
                 launch_events.append((e0, e1))
-            for t in (b, o, st):  # caller-stream allocations used on the slot's stream
+            for t in (*bs, *os_, *sts):  # caller-stream allocations used on the slot's stream
                 if isinstance(t, torch.Tensor) and t.is_cuda:
                     t.record_stream(s)
         for _, s in slots:
@@ -206,7 +252,7 @@ class BatchSolver:
     def inflight_stats(self, reset: bool = False) -> dict:
         """stats() summed over the solve_inflight slots' workspaces."""
         tot = None
-        for solver, s in getattr(self, "_slots", [(self, None)]):
+        for solver, s in (self._slots or [(self, None)]):
             st = solver.stats(reset=reset, stream=s)
             tot = st if tot is None else {k: (tot[k] + v if k != "best" else min(tot[k], v)) for k, v in st.items()}
         return tot

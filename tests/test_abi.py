@@ -112,3 +112,18 @@ def test_solve_batch_grid_arguments():
     assert f(16, 16, 16, 1, 16, 0, 0, None, -1) == -2
     assert f(None, None, None, 0, None, 0, 0, None, 2) == 0
     assert f(None, None, None, 0, None, 7, 0, None, 2) == -2  # unknown order
+
+
+def test_plane_tuning_rejects_oversized_chunks():
+    """A claimed chunk is staged and converted in one go, so at most 64
+    boards: larger chunk values are refused, nothing changed.
+    Host-side only (no GPU call)."""
+    from sudoku_solver_distributed_amd import _lib
+    L = _lib.load()
+    try:
+        assert L.sdk_set_plane_tuning(-1, -1, -1, 65) == -1
+        assert L.sdk_set_plane_tuning(-1, -1, -1, 255) == -1
+        assert L.sdk_set_plane_tuning(-1, -1, -1, 64) == 0
+        assert L.sdk_set_plane_tuning(-1, -1, -1, 0) == 0
+    finally:
+        L.sdk_set_plane_tuning(-1, -1, -1, -1)

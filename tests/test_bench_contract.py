@@ -14,9 +14,15 @@ def test_default_kernel_has_matching_pmc_profile():
     assert os.path.exists(path), path
     with open(path) as f:
         pmc = json.load(f)
-    # bench.py defaults: --batch 2^20, --seed 2024
+    # bench.py defaults at N = 1: --batch 2^20 boards per step, --seed 2024,
+    # one step per launch, 3 launches in flight at 2 waves per SIMD -- the
+    # counters must come from the launch shape the bench times (bench.py
+    # nulls roofline.frac / traffic otherwise)
+    from sudoku_solver_distributed_amd.solver import GRID_WAVES_INFLIGHT
     assert pmc["kernel"] == kname
-    assert pmc["batch"] == 1 << 20 and pmc["seed"] == 2024
+    assert pmc["seed"] == 2024 and pmc.get("workload", "hard17") == "hard17"
+    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": 3, "grid_waves": GRID_WAVES_INFLIGHT}
+    assert pmc["counters_per_launch"]["SQ_WAVES"] == 256 * 4 * GRID_WAVES_INFLIGHT
     assert pmc["valu_insts_per_launch"] > 0
     assert pmc["hbm_bytes_per_launch"] is None or pmc["hbm_bytes_per_launch"] > 0
 
@@ -61,6 +67,10 @@ def test_bench_two_rank_path_runs():
     lines = [l for l in outs[0].splitlines() if l.startswith("{")]
     assert len(lines) == 1 and not [l for l in outs[1].splitlines() if l.startswith("{")]
     d = json.loads(lines[0])
-    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 1 << 21 and d["config"]["dist_backend"] == "gloo"
+    # strong scaling (the default): the 2^20-board step split over the two
+    # ranks, each rank's launches holding two steps' shards
+    assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["dist_backend"] == "gloo"
+    assert d["config"]["global_batch"] == 1 << 20 and d["config"]["boards_per_gpu_per_step"] == 1 << 19
+    assert d["config"]["steps_per_launch"] == 2 and d["roofline"]["kernel"] == "plane_kernel_multi"
     assert d["side_configs"]["pathological"]["ranks"] == 2 and d["side_configs"]["pathological"]["identical"]
     assert d["all_solved_and_checked"] and d["value"] > 0

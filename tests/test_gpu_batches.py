@@ -1,0 +1,116 @@
+"""Several batches per launch (sdk_solve_batches / BatchSolver.solve_batches,
+the strong-scaling steps): every batch's bytes and statuses equal what
+solve() gives it alone -- the queue runs over the batches laid end to end, so
+claims, static hand-out windows, staged spans, the outbox, the wave-wide and
+restart tails and the deferred list all cross batch boundaries here."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import b81
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+FULL = "897124635531679284642385179154293867289716453376458912923867541765941328418532796"
+# givens repeating a digit in a row (rules B/C unsound: the deferred list)
+CLASH = "88" + FULL[2:30] + "0" + FULL[31:50] + "0" + FULL[51:70] + "0" + FULL[71:]
+
+
+def _mixed(seed):
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch, hard_search_batch
+    bad = hard17_batch(701, seed=seed).clone()
+    bad[3, 40] = 12                     # an invalid byte
+    bad[500] = torch.tensor(b81(CLASH), dtype=torch.uint8)
+    blank = torch.zeros((3, 81), dtype=torch.uint8)
+    return [b.contiguous().cuda() for b in (
+        hard17_batch(40_001, seed=seed + 1), generate_batch(3000, 55, seed=seed + 2).cpu(),
+        torch.empty((0, 81), dtype=torch.uint8), hard_search_batch(20_000, seed=seed + 3),
+        hard17_batch(1, seed=seed + 4), bad, blank, hard17_batch(9_003, seed=seed + 5))]
+
+
+def _check_same(solver, batches, order="gen", grid_waves=0):
+    want = [tuple(t.clone() for t in solver.solve(b, order=order)) for b in batches]
+    outs = [torch.full_like(b, 0xEE) for b in batches]
+    sts = [torch.full((b.shape[0],), 77, dtype=torch.int32, device=b.device) for b in batches]
+    solver.stats(reset=True)
+    got = solver.solve_batches(batches, outs, sts, order=order, grid_waves=grid_waves)
+    torch.cuda.synchronize()
+    for i, ((ws, wt), (gs, gt)) in enumerate(zip(want, got)):
+        assert torch.equal(ws, gs) and torch.equal(wt, gt), (order, grid_waves, i)
+    assert solver.stats()["finished"] == sum(b.shape[0] for b in batches)
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_solve_batches_matches_solve(solver, order):
+    batches = _mixed(100)
+    for gw in (0, 1):
+        _check_same(solver, batches, order, gw)
+
+
+def test_solve_batches_sixteen_unaligned(solver):
+    """16 batches of odd sizes (byte offsets of every batch boundary mod 4
+    differ), a grid of 1 wave per SIMD so most boards arrive by claims that
+    straddle batch boundaries, and views into one buffer at odd offsets."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    big = torch.cat([hard17_batch(200_000, seed=7), hard_search_batch(30_000, seed=8)]).cuda()
+    sizes = [1, 63, 65, 8191, 13, 20_011, 3, 40_000, 127, 1, 12_345, 77, 30_001, 5, 64, 50_000]
+    offs = np.cumsum([0] + sizes)
+    batches = [big[offs[i] + 3 * i: offs[i + 1] + 3 * i] for i in range(16)]
+    _check_same(solver, batches, "gen", 1)
+    _check_same(solver, batches, "node", 2)
+
+
+def test_solve_batches_restart_tail(solver):
+    """The restart tail (tail_mode 0: a drained wave's last boards restarted
+    on the wave-per-board solver) and the widest tail, through several batches."""
+    lib = solver.lib
+    try:
+        assert lib.sdk_set_plane_tuning(-1, 40, 0, -1) == 0
+        _check_same(solver, _mixed(200), "gen", 1)
+        assert lib.sdk_set_plane_tuning(-1, 40, 1, 1) == 0   # one-board claims
+        _check_same(solver, _mixed(300), "node", 0)
+    finally:
+        lib.sdk_set_plane_tuning(-1, -1, -1, -1)
+
+
+def test_solve_batches_vs_oracle(solver):
+    """Independent of solve(): hard boards split over 5 batches equal the
+    oracle's unique completions; generated boards the literal walk."""
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch
+    h = hard17_batch(12_000, seed=61)
+    g = generate_batch(2_000, 50, seed=62).cpu()
+    parts = [h[:5000], g[:1000], h[5000:11_000], g[1000:], h[11_000:]]
+    batches = [p.contiguous().cuda() for p in parts]
+    outs = [torch.empty_like(b) for b in batches]
+    sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in batches]
+    got = solver.solve_batches(batches, outs, sts, grid_waves=1)
+    torch.cuda.synchronize()
+    wh, cnt = O.solve_unique_batch(h.numpy())
+    wg, wgs = O.solve_batch(g.numpy())
+    want = [wh[:5000], wg[:1000], wh[5000:11_000], wg[1000:], wh[11_000:]]
+    for (s, t), w in zip(got, want):
+        assert np.array_equal(s.cpu().numpy(), w)
+    assert (cnt == 1).all() and all(bool((t == 1).all()) for _, t in got[::2])
+
+
+def test_solve_inflight_grouped(solver):
+    """solve_inflight(group=G): G consecutive batches per launch, launches in
+    flight on three slots -- the bench's strong-scaling steps -- equal solve()."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    steps = [hard17_batch(16_384 + 7 * i, seed=70 + i, device="cuda:0") for i in range(11)]
+    want = [tuple(t.clone() for t in solver.solve(b)) for b in steps]
+    outs = [torch.empty_like(b) for b in steps]
+    sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in steps]
+    ev = []
+    got = solver.solve_inflight(steps, outs, sts, inflight=3, group=4, launch_events=ev)
+    torch.cuda.synchronize()
+    assert len(ev) == 3  # 4 + 4 + 3 batches
+    for (ws, wt), (gs, gt) in zip(want, got):
+        assert torch.equal(ws, gs) and torch.equal(wt, gt)
+    with pytest.raises(ValueError):
+        solver.solve_inflight(steps, outs, sts, group=17)
+    with pytest.raises(ValueError):
+        solver.solve_inflight(steps, outs, sts, group=2, ordered=True)
+    with pytest.raises(ValueError):
+        solver.solve_batches(steps[:1] * 17, outs[:1] * 17, sts[:1] * 17)
