@@ -95,14 +95,14 @@ struct PlaneStack {
         asm("" : "+v"(x));
         return x;
     }
-    __device__ __forceinline__ void push(uint32_t level, const plane::Board &B, uint32_t entry) const
+    __device__ __forceinline__ void push(uint32_t level, plane::Board &B, uint32_t entry) const
     {
         const int v = (int)voff(level);
-#define PQ(a, b, c, d) (sdk_v4u){opaque(B.P[a / 3][a % 3]), opaque(B.P[b / 3][b % 3]), opaque(B.P[c / 3][c % 3]), \
-                                 opaque(B.P[d / 3][d % 3])}
+        plane::pin_board(B);
+#define PQ(a, b, c, d) (sdk_v4u){B.P[a / 3][a % 3], B.P[b / 3][b % 3], B.P[c / 3][c % 3], B.P[d / 3][d % 3]}
         const sdk_v4u q0 = PQ(0, 1, 2, 3), q1 = PQ(4, 5, 6, 7), q2 = PQ(8, 9, 10, 11), q3 = PQ(12, 13, 14, 15),
                       q4 = PQ(16, 17, 18, 19), q5 = PQ(20, 21, 22, 23),
-                      q6 = (sdk_v4u){opaque(B.P[8][0]), opaque(B.P[8][1]), opaque(B.P[8][2]), entry};
+                      q6 = (sdk_v4u){B.P[8][0], B.P[8][1], B.P[8][2], entry};
 #undef PQ
         __builtin_amdgcn_raw_buffer_store_b128(q0, rsrc, v, 0, 0);
         __builtin_amdgcn_raw_buffer_store_b128(q1, rsrc, v, 16, 0);
@@ -1036,7 +1036,14 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             state = PL_SOLVED;
             if (best)
                 __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        } else if (r == plane::STUCK) {
+        }
+        // a guess (push) or a backtrack (pop) both end by fixing one cell to
+        // one digit: set_cell runs once for both groups of lanes (the wave
+        // runs both paths in most iterations)
+        bool fix = false;
+        int fix_band = 0, fix_pos = 0;
+        uint32_t fix_d = 0;
+        if (r == plane::STUCK) {
             if (depth == PLANE_MAX_DEPTH) {
                 plane_defer(io.stat(p), p, ws, defer_list);  // too deep for the stack: the wave kernel's
                 fin--;
@@ -1046,15 +1053,11 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
                 state = PL_CANCELLED;
             } else {
-                int band, pos;
-                plane::pick_cell(und, node_order, band, pos);
-                const uint32_t cand = plane::cell_cand(B, band, pos);
-                const uint32_t d = cand & (0u - cand);
-                stk.push(depth, B, plane::make_entry(band, pos, cand ^ d));
-                depth++;
-                guesses++;
-                bguess++;
-                plane::set_cell(B, band, pos, d);
+                plane::pick_cell(und, node_order, fix_band, fix_pos);
+                const uint32_t cand = plane::cell_cand(B, fix_band, fix_pos);
+                fix_d = cand & (0u - cand);
+                stk.push(depth, B, plane::make_entry(fix_band, fix_pos, cand ^ fix_d));
+                fix = true;
             }
         } else if (r == plane::DEAD) {
             // back to the deepest level with an untried digit
@@ -1080,12 +1083,18 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 #endif
                 B.Det[0] = B.Det[1] = B.Det[2] = 0;
                 stk.put_entry(depth, e & ~(d << 8));
-                depth++;
-                guesses++;
-                bguess++;
-                plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
+                fix_band = (int)((e >> 5) & 3u);
+                fix_pos = (int)(e & 31u);
+                fix_d = d;
+                fix = true;
                 break;
             }
+        }
+        if (fix) {
+            depth++;
+            guesses++;
+            bguess++;
+            plane::set_cell(B, fix_band, fix_pos, fix_d);
         }
     }
     if (ob_count) plane_flush_outbox(outbox, ob_count, lane, io);

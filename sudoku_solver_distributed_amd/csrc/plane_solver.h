@@ -281,12 +281,20 @@ PS_FN void pick_cell(const uint32_t und[3], int node_order, int &band, int &pos)
 
 PS_FN uint32_t band_word(const uint32_t (&w)[3], int band) { return band == 0 ? w[0] : band == 1 ? w[1] : w[2]; }
 
-// candidates (bit d = digit d+1) of the cell at (band, pos)
+// candidates (bit d = digit d+1) of the cell at (band, pos).  Branch-free
+// (band and pos differ per lane): the cell's bit of digit d's three words
+// under a one-hot band mask, shifted down to bit 0, accumulated from digit 8
+// down as c = 2c + bit -- right shifts and adds only, the full-rate forms.
 PS_FN uint32_t cell_cand(const Board &B, int band, int pos)
 {
+    const uint32_t cb = 1u << pos;
+    const uint32_t m0 = band == 0 ? cb : 0u, m1 = band == 1 ? cb : 0u, m2 = band == 2 ? cb : 0u;
     uint32_t c = 0;
 #pragma unroll
-    for (int d = 0; d < 9; ++d) c |= ((band_word(B.P[d], band) >> pos) & 1u) << d;
+    for (int d = 8; d >= 0; --d) {
+        const uint32_t x = or_and(or_and(B.P[d][0] & m0, B.P[d][1], m1), B.P[d][2], m2);
+        c = c + c + (x >> pos);
+    }
     return c;
 }
 
