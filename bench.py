@@ -365,6 +365,9 @@ def main():
                          "default, 2 with launches in flight, a full grid at --inflight 1; 0: a full grid)")
     ap.add_argument("--launch-events", action="store_true",
                     help="also time each launch's own span with events on its slot stream (launch_ms)")
+    ap.add_argument("--mrv-after", type=int, default=-1,
+                    help="passes on a board before its search switches to the completion count "
+                         "(sdk_set_plane_search; -1: the library default, 0: the walk's order only) -- A/B only")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the configs[1] / configs[3] side measurements")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -398,6 +401,8 @@ def main():
     from sudoku_solver_distributed_amd.solver import get_solver
 
     solver = get_solver(dev)
+    if args.mrv_after >= 0:
+        solver.lib.sdk_set_plane_search(args.mrv_after)
     make = hard17_batch if args.workload == "hard17" else hard_search_batch
     if args.scaling == "strong":
         lo, hi = shard_bounds(args.batch, rank, world)

@@ -191,6 +191,17 @@ int sdk_set_solve_kernel(int kernel);
  * them.  Returns 0, or -1 for an out-of-range value (nothing changed). */
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk);
 
+/* Plane-kernel search (library extension, no reference counterpart): a
+ * board still searching after `mrv_after` propagation passes goes back to
+ * its propagated root and counts its completions (to two) branching on
+ * fewest-candidates cells: exactly one completion is the walk's answer, none
+ * means none for the walk too, two send the board back to the walk's own
+ * branch order.  0 keeps every board on the walk's order; -1
+ * restores the default ($SDK_PLANE_MRV, built-in 128).  Results never
+ * depend on it.  Returns the previous setting (-1: default), -1 for an
+ * out-of-range value (nothing changed). */
+int sdk_set_plane_search(int mrv_after);
+
 /* Library / device info. */
 const char *sdk_last_error(void);
 const char *sdk_version(void);

@@ -41,6 +41,7 @@ EXPORTS = (
     "sdk_device_cu_count",
     "sdk_set_solve_kernel",
     "sdk_set_plane_tuning",
+    "sdk_set_plane_search",
 )
 SDK_KERNELS = {"auto": 1, "packed": 5, "plane": 6}
 SDK_MAX_BATCHES = 16  # sdk_solve_batches: batches per launch
@@ -98,6 +99,8 @@ def load() -> ctypes.CDLL:
     L.sdk_set_solve_kernel.argtypes = [i32]
     L.sdk_set_plane_tuning.restype = i32
     L.sdk_set_plane_tuning.argtypes = [i32, i32, i32, i32]
+    L.sdk_set_plane_search.restype = i32
+    L.sdk_set_plane_search.argtypes = [i32]
     _lib = L
     return L
 

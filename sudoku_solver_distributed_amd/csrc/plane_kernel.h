@@ -52,6 +52,11 @@
 #ifndef SDK_PLANE_CHUNK
 #define SDK_PLANE_CHUNK 64
 #endif
+// passes on a board before its search switches from the walk's branch order
+// to the completion count (plane::search_step; 0: never)
+#ifndef SDK_PLANE_MRV
+#define SDK_PLANE_MRV 128
+#endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
 #endif
@@ -60,10 +65,6 @@
 // its boards and deposits them one at a time by ballots
 #ifndef SDK_PLANE_PRECONV
 #define SDK_PLANE_PRECONV 1
-#endif
-// 1: a backtrack loads the level's whole stack line in one round trip
-#ifndef SDK_PLANE_POP1
-#define SDK_PLANE_POP1 1
 #endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
@@ -127,7 +128,8 @@ struct PlaneStack {
     }
     // the whole line in one round trip: the entry (last quad) decides whether
     // the level still has a digit; if not (rare), the planes go unused
-    __device__ __forceinline__ sdk_v4u pop(uint32_t level, plane::Board &B) const
+    __device__ __forceinline__ uint32_t pop(uint32_t level, plane::Board &B) const { return pop_line(level, B)[3]; }
+    __device__ __forceinline__ sdk_v4u pop_line(uint32_t level, plane::Board &B) const
     {
         const int v = (int)voff(level);
         const sdk_v4u q0 = __builtin_amdgcn_raw_buffer_load_b128(rsrc, v, 0, 0);
@@ -491,7 +493,7 @@ __device__ __forceinline__ void plane_flush_outbox(const uint32_t *outbox, uint3
 // a record per handed-over board in the wave's staging area (stride: odd, so
 // 64 lanes writing one word each hit 64 banks): 27 plane words, board index
 // lo / hi, depth, stack line offset, guesses so far
-enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = 40 };
+enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = 40 };  // word 32: the board's search mode (mst)
 // the last record, read up to word 48 (pad lanes), stays below the zero byte
 static_assert((PLANE_TAIL_MAX - 1) * PLANE_TAIL_REC + 48 < PLANE_STAGE_DWORDS - 1, "tail records");
 
@@ -531,7 +533,7 @@ template <class IO>
 __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
                                              const IO &io, unsigned long long *__restrict__ ws,
                                              int64_t *__restrict__ defer_list, const int64_t *best, int node_order,
-                                             uint32_t (&st)[5])
+                                             uint32_t mrv_after, uint32_t (&st)[5])
 {
     const wide::Lanes L = wide::lanes();
     const int c0 = plane_slot_cell(lane, 0), c1 = plane_slot_cell(lane, 1);
@@ -547,9 +549,11 @@ __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int
         const WideStack stk = {stack_rsrc, (uint32_t)__builtin_amdgcn_readfirstlane(rec[30]),
                                L.valid ? 4u * L.word : 108u, L.valid, lane == 48};
         wide::Stats ws_ = {0u, 0u, (uint32_t)__builtin_amdgcn_readfirstlane(rec[31])};
-        const int r = wide::solve(w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_, [&] {
-            return best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pb;
-        });
+        uint32_t mst = __builtin_amdgcn_readfirstlane(rec[32]);
+        const int r = wide::solve(
+            w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_,
+            [&] { return best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pb; }, mst,
+            mrv_after);
         passes += ws_.passes;
         guesses += ws_.guesses;
         const uint8_t *src = io.src(pb);
@@ -614,7 +618,8 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 template <class IO>
 __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__restrict__ ws,
                                            uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list,
-                                           int ordered, int order, int refill, int tail, int tail_mode, int chunk)
+                                           int ordered, int order, int refill, int tail, int tail_mode, int chunk,
+                                           uint32_t mrv_after)
 {
     const int64_t n = io.total();  // boards of the launch (virtual indices 0..n-1)
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
@@ -644,6 +649,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     // over the wave at exit)
     uint32_t fin = 0, solved = 0, guesses = 0, passes = 0, deferred = 0;
     uint32_t bguess = 0;  // guesses on the current board (dropped if it is handed off)
+    uint32_t mst = 0;     // the board's search mode and pass count (plane::search_step)
     bool drained = false;  // the queue is empty and this wave's reservoir too
     // Board hand-out.  The first nt boards go out statically, 64 consecutive
     // ones per wave; the rest through the queue head (board nt + head).  A
@@ -691,6 +697,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                 p = q;
                 depth = 0;
                 bguess = 0;
+                mst = 0;
                 state = PL_ACTIVE;
             } else {
                 for (int i = 0; i < 81; ++i) io.out[q * 81 + i] = src[i];  // raw input back
@@ -720,6 +727,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     p = q;
                     depth = 0;
                     bguess = 0;
+                    mst = 0;
                     state = PL_ACTIVE;
                 } else {
                     const uint8_t *src = io.src(q);
@@ -904,6 +912,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                         p = (IO::multi ? rec_id + ((int64_t)base - rec_base) : (int64_t)base) + (int64_t)rank;
                         depth = 0;
                         bguess = 0;
+                        mst = 0;
                         if (!bad && !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
                             plane::planes_from_slices(B, V, given);
                             state = PL_ACTIVE;
@@ -976,6 +985,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                         p = io.id((int64_t)base) + (int64_t)lanes_below(loaded);
                         depth = 0;
                         bguess = 0;
+                        mst = 0;
                         if (!((bad >> lane) & 1u) &&
                             !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
                             uint32_t V[4][3], given[3];
@@ -1032,69 +1042,27 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         passes++;
         uint32_t und[3];
         const int r = plane::pass(B, und);
-        if (r == plane::SOLVED) {
+        if (r == plane::STUCK && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
+            state = PL_CANCELLED;  // ordered mode: a lower board is solved
+            continue;
+        }
+        // guess / backtrack / search-mode switch (plane::search_step: the
+        // lane solver's own step, checked on the host against the oracle)
+        const uint32_t gb = bguess;
+        const int s = plane::search_step(B, und, r, depth, mst, stk, node_order, PLANE_MAX_DEPTH, mrv_after, bguess);
+        guesses += bguess - gb;
+        if (s == plane::S_SOLVED) {
             state = PL_SOLVED;
             if (best)
                 __hip_atomic_fetch_min((int64_t *)&ws[WS_BEST], p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        // a guess (push) or a backtrack (pop) both end by fixing one cell to
-        // one digit: set_cell runs once for both groups of lanes (the wave
-        // runs both paths in most iterations)
-        bool fix = false;
-        int fix_band = 0, fix_pos = 0;
-        uint32_t fix_d = 0;
-        if (r == plane::STUCK) {
-            if (depth == PLANE_MAX_DEPTH) {
-                plane_defer(io.stat(p), p, ws, defer_list);  // too deep for the stack: the wave kernel's
-                fin--;
-                deferred++;
-                guesses -= bguess;
-                state = PL_IDLE;
-            } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
-                state = PL_CANCELLED;
-            } else {
-                plane::pick_cell(und, node_order, fix_band, fix_pos);
-                const uint32_t cand = plane::cell_cand(B, fix_band, fix_pos);
-                fix_d = cand & (0u - cand);
-                stk.push(depth, B, plane::make_entry(fix_band, fix_pos, cand ^ fix_d));
-                fix = true;
-            }
-        } else if (r == plane::DEAD) {
-            // back to the deepest level with an untried digit
-            for (;;) {
-                if (depth == 0) {
-                    state = PL_UNSOLVABLE;
-                    break;
-                }
-                depth--;
-#if SDK_PLANE_POP1
-                const sdk_v4u t = stk.pop(depth, B);
-                const uint32_t e = t[3];
-                const uint32_t rem = (e >> 8) & 0x1FFu;
-                if (!rem) continue;
-                const uint32_t d = rem & (0u - rem);
-#else
-                const sdk_v4u t = stk.top(depth);
-                const uint32_t e = t[3];
-                const uint32_t rem = (e >> 8) & 0x1FFu;
-                if (!rem) continue;
-                const uint32_t d = rem & (0u - rem);
-                stk.restore(depth, B, t);
-#endif
-                B.Det[0] = B.Det[1] = B.Det[2] = 0;
-                stk.put_entry(depth, e & ~(d << 8));
-                fix_band = (int)((e >> 5) & 3u);
-                fix_pos = (int)(e & 31u);
-                fix_d = d;
-                fix = true;
-                break;
-            }
-        }
-        if (fix) {
-            depth++;
-            guesses++;
-            bguess++;
-            plane::set_cell(B, fix_band, fix_pos, fix_d);
+        } else if (s == plane::S_NONE) {
+            state = PL_UNSOLVABLE;
+        } else if (s == plane::S_DEEP) {
+            plane_defer(io.stat(p), p, ws, defer_list);  // too deep for the stack: the wave kernel's
+            fin--;
+            deferred++;
+            guesses -= bguess;
+            state = PL_IDLE;
         }
     }
     if (ob_count) plane_flush_outbox(outbox, ob_count, lane, io);
@@ -1119,11 +1087,12 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             rec[29] = depth;
             rec[30] = stk.lane_off;
             rec[31] = bguess;
+            rec[32] = mst;
         }
         wave_lds_sync();
         uint32_t wst[5];
         plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, io, ws, defer_list, best, node_order,
-                        wst);
+                        mrv_after, wst);
 #if SDK_PLANE_STAMPS
         st_tailp = wst[2];
 #endif
@@ -1186,19 +1155,19 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int tail_mode, int chunk)
+    int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after)
 {
     const PlaneIO1 io = {puzzles, sols, status, n};
-    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk);
+    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk, mrv_after);
 }
 
 // several batches, one queue over them (sdk_solve_batches; unordered)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel_multi(
     const PlaneBatches bs, unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack,
-    int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk)
+    int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after)
 {
     const PlaneIOn io = {bs};
-    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk);
+    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk, mrv_after);
 }
 
 #endif  // SDK_PLANE_KERNEL_H

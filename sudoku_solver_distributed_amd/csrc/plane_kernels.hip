@@ -17,15 +17,25 @@
 // PLANE_TAIL_MAX), $SDK_PLANE_TAIL_MODE that solver (1: the wave-wide solver
 // continues each search, 0: the wave-per-board solver restarts it),
 // $SDK_PLANE_CHUNK most boards a wave claims from the queue at once (0: one
-// claim per refill)
+// claim per refill), $SDK_PLANE_MRV passes on a board before its search
+// switches to the completion count (plane::search_step; 0: never)
 static int env_int(const char *name, int dflt)
 {
     const char *e = getenv(name);
     return e && e[0] ? atoi(e) : dflt;
 }
 
-// sdk_set_plane_tuning overrides (-1: the environment's / built-in default)
-static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1};
+// sdk_set_plane_tuning / sdk_set_plane_search overrides (-1: the
+// environment's / built-in default)
+static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1}, g_mrv{-1};
+
+int sdk_set_plane_search(int mrv_after)
+{
+    if (mrv_after > (int)plane::MST_PASSES) return -1;
+    const int prev = g_mrv.load();
+    g_mrv = mrv_after < 0 ? -1 : mrv_after;
+    return prev;
+}
 
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 {
@@ -43,6 +53,7 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 
 struct PlaneKnobs {
     int refill, tail, tail_mode, chunk;
+    uint32_t mrv_after;
 };
 
 static PlaneKnobs plane_knobs()
@@ -51,13 +62,16 @@ static PlaneKnobs plane_knobs()
     static const int tail_env = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
     static const int tail_mode_env = env_int("SDK_PLANE_TAIL_MODE", SDK_PLANE_TAIL_MODE);
     static const int chunk_env = env_int("SDK_PLANE_CHUNK", SDK_PLANE_CHUNK);
+    static const int mrv_env = env_int("SDK_PLANE_MRV", SDK_PLANE_MRV);
     const int refill = g_refill >= 0 ? g_refill.load() : refill_env;
     int tail = g_tail >= 0 ? g_tail.load() : tail_env;
     tail = tail > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail;
     const int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : tail_mode_env;
     int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
     chunk = chunk > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : chunk;  // ($SDK_PLANE_CHUNK is not range-checked)
-    return {refill, tail, tail_mode, chunk};
+    int mrv = g_mrv >= 0 ? g_mrv.load() : mrv_env;
+    mrv = mrv < 0 ? 0 : mrv > (int)plane::MST_PASSES ? (int)plane::MST_PASSES : mrv;
+    return {refill, tail, tail_mode, chunk, (uint32_t)mrv};
 }
 
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
@@ -67,7 +81,7 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
     const PlaneKnobs k = plane_knobs();
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk);
+                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);
     return hipGetLastError();
 }
 
@@ -77,7 +91,7 @@ hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws
     const PlaneKnobs k = plane_knobs();
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel_multi, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, bs, ws, stack,
-                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk);
+                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);
     return hipGetLastError();
 }
 

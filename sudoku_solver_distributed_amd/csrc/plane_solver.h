@@ -39,8 +39,10 @@
 
 #ifdef __HIPCC__
 #define PS_FN __host__ __device__ __forceinline__
+#define PS_MF __host__ __device__ __forceinline__
 #else
 #define PS_FN static inline
+#define PS_MF inline
 #endif
 
 #if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
@@ -279,6 +281,43 @@ PS_FN void pick_cell(const uint32_t und[3], int node_order, int &band, int &pos)
     }
 }
 
+// Fewest-candidates cell for the completion count (search mode M_COUNT
+// below): the first undetermined cell (band order, then bit order) with
+// exactly 2 candidates, else with exactly 3, else the first undetermined
+// cell.  Saturating candidate counters over the nine planes, per band.
+// the choice from the per-band masks of undetermined cells with exactly 2
+// (e2) and exactly 3 (e3) candidates (shared with the wave-wide solver)
+PS_FN void pick_mrv_masks(const uint32_t (&e2)[3], const uint32_t (&e3)[3], const uint32_t und[3], int &band,
+                          int &pos)
+{
+    const uint32_t w[3] = {e2[0] ? e2[0] : e3[0] ? e3[0] : und[0], e2[1] ? e2[1] : e3[1] ? e3[1] : und[1],
+                           e2[2] ? e2[2] : e3[2] ? e3[2] : und[2]};
+    const int k2 = e2[0] ? 0 : e2[1] ? 1 : e2[2] ? 2 : -1;
+    const int k3 = e3[0] ? 0 : e3[1] ? 1 : e3[2] ? 2 : -1;
+    band = k2 >= 0 ? k2 : k3 >= 0 ? k3 : (und[0] ? 0 : und[1] ? 1 : 2);
+    pos = __builtin_ctz(band == 0 ? w[0] : band == 1 ? w[1] : w[2]);
+}
+
+PS_FN void pick_mrv(const Board &B, const uint32_t und[3], int &band, int &pos)
+{
+    uint32_t e2[3], e3[3];
+#pragma unroll
+    for (int b = 0; b < 3; ++b) {
+        uint32_t c1 = 0, c2 = 0, c3 = 0, c4 = 0;
+#pragma unroll
+        for (int d = 0; d < 9; ++d) {
+            const uint32_t p = B.P[d][b];
+            c4 = or_and(c4, c3, p);
+            c3 = or_and(c3, c2, p);
+            c2 = or_and(c2, c1, p);
+            c1 |= p;
+        }
+        e2[b] = and_andn(und[b], c2, c3);
+        e3[b] = and_andn(und[b], c3, c4);
+    }
+    pick_mrv_masks(e2, e3, und, band, pos);
+}
+
 PS_FN uint32_t band_word(const uint32_t (&w)[3], int band) { return band == 0 ? w[0] : band == 1 ? w[1] : w[2]; }
 
 // candidates (bit d = digit d+1) of the cell at (band, pos).  Branch-free
@@ -455,6 +494,161 @@ enum { STACK_WORDS = 28, STACK_ENTRY = 27 };
 // branch entry: bits 0-4 pos, 5-6 band, 8-16 untried digits
 PS_FN uint32_t make_entry(int band, int pos, uint32_t rem) { return (uint32_t)pos | ((uint32_t)band << 5) | (rem << 8); }
 
+// ---- search modes of a board
+// M_WALK: branch on the walk's next cell, digits ascending -- the first
+// completion found is the walk's.  A board still searching
+// after `mrv_after` passes switches to M_COUNT: back to its propagated root
+// (stack level 0), branching on a fewest-candidates cell and counting
+// completions to two, the first one kept on the stack's last level.  Exactly
+// one completion IS the walk's answer (the walk's first completion is the
+// only one); none means none for the walk too; a second one sends the board
+// back to its root in M_FINAL, the walk again, with no further switch.
+// Results never depend on mrv_after (0 = never switch).  Heavy-tailed sets
+// gain most: 17-clue boards whose walk order is unlucky need up to ~5000
+// walk passes, and at most ~1100 this way.
+enum { M_WALK = 0, M_COUNT = 1, M_FINAL = 2 };
+
+// A board's search state besides its planes: depth, and `mst` = passes on
+// this board (bits 0-23) | mode << 24 | a completion kept (bit 26).
+enum : uint32_t { MST_PASSES = 0xFFFFFFu, MST_FOUND = 1u << 26 };
+PS_FN int mst_mode(uint32_t mst) { return (int)((mst >> 24) & 3u); }
+PS_FN uint32_t mst_set_mode(uint32_t mst, int mode) { return (mst & MST_PASSES) | ((uint32_t)mode << 24); }
+
+enum { S_CONT = 0, S_SOLVED = 1, S_NONE = 2, S_DEEP = 3 };
+
+// One search step after a pass with result r (the lane solver's, and the
+// plane kernel's lane loop: both call this).  Stack: push(level, B, entry),
+// pop(level, B) -> entry (the level's planes into B, entry with them),
+// put_entry(level, e).  Returns S_CONT (pass again), S_SOLVED
+// (B holds the answer), S_NONE (no completion) or S_DEEP (deeper than the
+// stack: the board goes to the wave kernel).  mrv_after: passes before the
+// switch to the completion count (0 never).  guesses: +1 per branch node.
+template <class Stack>
+PS_FN int search_step(Board &B, const uint32_t (&und)[3], int r, uint32_t &depth, uint32_t &mst, const Stack &stk,
+                      int node_order, uint32_t max_depth, uint32_t mrv_after, uint32_t &guesses)
+{
+    mst++;
+    const int mode = mst_mode(mst);
+    const uint32_t sol_level = max_depth - 1;  // M_COUNT keeps its first completion here
+    // every plane load of the step at one site (the end): the level whose
+    // planes replace the board's -- the next untried digit's, the root, or
+    // a kept completion (one site keeps the kernel's registers in bounds)
+    int reload = -1, save = -1;  // and the one plane store: a guess's level, or the kept completion
+    uint32_t save_entry = 0;
+    bool fix = false, fresh = false;
+    int fix_band = 0, fix_pos = 0, res = S_CONT;
+    uint32_t fix_d = 0;
+    if (mode == M_WALK && mrv_after && r != SOLVED && (mst & MST_PASSES) >= mrv_after) {
+        reload = depth ? 0 : -1;  // the propagated root (level 0's planes)
+        fresh = true;
+        depth = 0;
+        mst = mst_set_mode(mst, M_COUNT);
+        r = OPEN;
+    }
+    if (r == SOLVED) {
+        if (mode != M_COUNT) return S_SOLVED;
+        if (mst & MST_FOUND) {  // a second completion: the walk decides, from the root
+            reload = 0;
+            depth = 0;
+            mst = mst_set_mode(mst, M_FINAL);
+            r = OPEN;
+        } else {
+            mst |= MST_FOUND;
+            save = (int)sol_level;
+            r = DEAD;  // and look for another
+        }
+    }
+    if (r == STUCK) {
+        if (depth == (mode == M_COUNT ? sol_level : max_depth)) {
+            if (mode != M_COUNT) return S_DEEP;
+            reload = 0;  // too deep to count: the walk, from the root
+            depth = 0;
+            mst = mst_set_mode(mst, M_FINAL);
+        } else {
+            if (mode == M_COUNT) pick_mrv(B, und, fix_band, fix_pos);
+            else pick_cell(und, node_order, fix_band, fix_pos);
+            const uint32_t cand = cell_cand(B, fix_band, fix_pos);
+            fix_d = cand & (0u - cand);
+            save = (int)depth;
+            save_entry = make_entry(fix_band, fix_pos, cand ^ fix_d);
+            fix = true;
+        }
+    }
+    // DEAD: back to the deepest level with an untried digit, scanning down
+    // from depth - 1 (each level's planes and entry in one load)
+    bool scan = false;
+    if (r == DEAD) {
+        if (depth) {
+            scan = true;
+            reload = (int)depth - 1;
+        } else {
+            if (mode != M_COUNT || !(mst & MST_FOUND)) return S_NONE;
+            reload = (int)sol_level;  // exactly one completion
+            res = S_SOLVED;
+        }
+    }
+    if (save >= 0) stk.push((uint32_t)save, B, save_entry);
+    if (reload >= 0 || fresh) B.Det[0] = B.Det[1] = B.Det[2] = 0;
+    while (reload >= 0) {
+        const uint32_t e = stk.pop((uint32_t)reload, B);
+        if (!scan) break;
+        const uint32_t rem = (e >> 8) & 0x1FFu;
+        if (rem) {
+            fix_d = rem & (0u - rem);
+            stk.put_entry((uint32_t)reload, e & ~(fix_d << 8));
+            fix_band = (int)((e >> 5) & 3u);
+            fix_pos = (int)(e & 31u);
+            depth = (uint32_t)reload;
+            fix = true;
+            break;
+        }
+        if (reload == 0) {  // the search is exhausted
+            if (mode == M_COUNT && (mst & MST_FOUND)) {  // exactly one completion
+                reload = (int)sol_level;
+                scan = false;
+                res = S_SOLVED;
+                continue;
+            }
+            return S_NONE;
+        }
+        reload--;
+    }
+    // a guess and a backtrack both end by fixing one cell to one digit: one
+    // set_cell for both groups of lanes (the wave runs both paths in most
+    // iterations)
+    if (fix) {
+        depth++;
+        guesses++;
+        set_cell(B, fix_band, fix_pos, fix_d);
+    }
+    return res;
+}
+
+// the step's stack interface over a word stack with put(level, k, v) / get(level, k)
+template <typename S>
+struct WordStack {
+    S &s;
+    PS_MF void push(uint32_t level, const Board &B, uint32_t entry) const
+    {
+        save(level, B);
+        s.put(level, STACK_ENTRY, entry);
+    }
+    PS_MF uint32_t pop(uint32_t level, Board &B) const
+    {
+        load(level, B);
+        return s.get(level, STACK_ENTRY);
+    }
+    PS_MF void put_entry(uint32_t level, uint32_t e) const { s.put(level, STACK_ENTRY, e); }
+    PS_MF void load(uint32_t level, Board &B) const
+    {
+        for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = s.get(level, w);
+    }
+    PS_MF void save(uint32_t level, const Board &B) const
+    {
+        for (int w = 0; w < 27; ++w) s.put(level, w, B.P[w / 3][w % 3]);
+    }
+};
+
 // Host / reference driver: solve one board in place with a stack of at
 // least max_depth levels.  Returns 1 solved, 0 no completion, -1 depth
 // overflow (board left to the wave kernel).
@@ -463,46 +657,17 @@ struct Stats {
 };
 
 template <typename Stack>
-PS_FN int solve(Board &B, Stack &stk, int node_order, uint32_t max_depth, Stats &st)
+PS_FN int solve(Board &B, Stack &stk, int node_order, uint32_t max_depth, Stats &st, uint32_t mrv_after = 0)
 {
-    uint32_t depth = 0;
+    const WordStack<Stack> ws = {stk};
+    uint32_t depth = 0, mst = 0;
     for (;;) {
         uint32_t und[3];
         const int r = pass(B, und);
         st.passes++;
-        if (r == SOLVED) return 1;
-        if (r == OPEN) continue;
-        if (r == STUCK) {
-            if (depth == max_depth) return -1;
-            int band, pos;
-            pick_cell(und, node_order, band, pos);
-            const uint32_t cand = cell_cand(B, band, pos);
-            const uint32_t d = cand & (0u - cand);
-#pragma unroll
-            for (int w = 0; w < 27; ++w) stk.put(depth, w, B.P[w / 3][w % 3]);
-            stk.put(depth, STACK_ENTRY, make_entry(band, pos, cand ^ d));
-            depth++;
-            st.guesses++;
-            set_cell(B, band, pos, d);
-            continue;
-        }
-        // DEAD: back to the deepest level with an untried digit
-        for (;;) {
-            if (depth == 0) return 0;
-            depth--;
-            const uint32_t e = stk.get(depth, STACK_ENTRY);
-            const uint32_t rem = (e >> 8) & 0x1FFu;
-            if (!rem) continue;
-            const uint32_t d = rem & (0u - rem);
-#pragma unroll
-            for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = stk.get(depth, w);
-            B.Det[0] = B.Det[1] = B.Det[2] = 0;
-            stk.put(depth, STACK_ENTRY, e & ~(d << 8));
-            depth++;
-            st.guesses++;
-            set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
-            break;
-        }
+        const int s = search_step(B, und, r, depth, mst, ws, node_order, max_depth, mrv_after, st.guesses);
+        if (s == S_CONT) continue;
+        return s == S_SOLVED ? 1 : s == S_NONE ? 0 : -1;
     }
 }
 

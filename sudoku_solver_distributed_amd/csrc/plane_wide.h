@@ -201,6 +201,28 @@ WD_FN void row_or_ge2(V &o, V &t)
     WD_STEP(8)
 #undef WD_STEP
 }
+// candidate counts over the row's nine digit lanes, saturating: t >= 2,
+// th >= 3, f >= 4 (row-uniform; o = the lane's word, pad lanes 0)
+WD_FN void row_count234(V o, V &t, V &th, V &f)
+{
+    t = V(0u);
+    th = V(0u);
+    f = V(0u);
+#define WD_STEP(N)                                                            \
+    {                                                                         \
+        const V o2 = ror<N>(o), t2 = ror<N>(t), h2 = ror<N>(th), f2 = ror<N>(f); \
+        f = or3(or3(f, f2, th & o2), t & t2, o & h2);                         \
+        th = or3(or3(th, h2, t & o2), o & t2, V(0u));                         \
+        t = or3(t, t2, o & o2);                                               \
+        o = o | o2;                                                           \
+    }
+    WD_STEP(1)
+    WD_STEP(2)
+    WD_STEP(4)
+    WD_STEP(8)
+#undef WD_STEP
+}
+
 WD_FN V row_or(V v)
 {
     v = v | ror<1>(v);
@@ -304,24 +326,64 @@ struct Stats {
 // stack) to its first completion in walk order.  Stack: push(level, w, L,
 // entry), entry(level), restore(level, L), put_entry(level, e) over the
 // plane_kernel stack line layout.  cancelled(): ordered mode, a lower board
-// has a completion.  Returns W_*; on W_SOLVED w holds the completion.
+// has a completion.  mst / mrv_after: the board's search mode, as the lane
+// solver's (plane::search_step, the same transitions).  Returns W_*; on
+// W_SOLVED w holds the completion.
 template <class Stack, class Cancel>
 WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int node_order, uint32_t max_depth,
-                Stats &st, Cancel cancelled)
+                Stats &st, Cancel cancelled, uint32_t &mst, uint32_t mrv_after)
 {
     V det = V(0u);
+    const uint32_t sol_level = max_depth - 1;
     for (;;) {
         V und;
         st.passes++;
-        const int r = pass(w, det, und, L);
+        int r = pass(w, det, und, L);
+        mst++;
+        const int mode = plane::mst_mode(mst);
+        if (mode == plane::M_WALK && mrv_after && r != SOLVED && (mst & plane::MST_PASSES) >= mrv_after) {
+            if (depth) w = stk.restore(0, L);  // the propagated root
+            det = V(0u);
+            depth = 0;
+            mst = plane::mst_set_mode(mst, plane::M_COUNT);
+            continue;
+        }
         if (r == OPEN) continue;
-        if (r == SOLVED) return W_SOLVED;
+        if (r == SOLVED) {
+            if (mode != plane::M_COUNT) return W_SOLVED;
+            if (mst & plane::MST_FOUND) {  // a second completion: the walk, from the root
+                w = stk.restore(0, L);
+                det = V(0u);
+                depth = 0;
+                mst = plane::mst_set_mode(mst, plane::M_FINAL);
+                continue;
+            }
+            mst |= plane::MST_FOUND;
+            stk.push(sol_level, w, L, 0u);
+            r = DEAD;
+        }
         if (r == STUCK) {
-            if (depth == max_depth) return W_OVERFLOW;
+            if (depth == (mode == plane::M_COUNT ? sol_level : max_depth)) {
+                if (mode != plane::M_COUNT) return W_OVERFLOW;
+                w = stk.restore(0, L);
+                det = V(0u);
+                depth = 0;
+                mst = plane::mst_set_mode(mst, plane::M_FINAL);
+                continue;
+            }
             if (cancelled()) return W_CANCELLED;
             const uint32_t u[3] = {rdl(und, 0), rdl(und, 16), rdl(und, 32)};
             int band, pos;
-            plane::pick_cell(u, node_order, band, pos);
+            if (mode == plane::M_COUNT) {
+                V t, th, f;
+                row_count234(pick(L.valid, w, V(0u)), t, th, f);
+                const V e2 = und & andn(t, th), e3 = und & andn(th, f);
+                const uint32_t m2[3] = {rdl(e2, 0), rdl(e2, 16), rdl(e2, 32)};
+                const uint32_t m3[3] = {rdl(e3, 0), rdl(e3, 16), rdl(e3, 32)};
+                plane::pick_mrv_masks(m2, m3, u, band, pos);
+            } else {
+                plane::pick_cell(u, node_order, band, pos);
+            }
             const uint64_t cm = ballot(mand(mand(L.valid, eq(L.b, V((uint32_t)band))), ne((w >> pos) & 1u, V(0u))));
             const uint32_t cand = (uint32_t)(cm >> (16 * band)) & 0x1FFu;
             const uint32_t dbit = cand & (0u - cand);
@@ -334,7 +396,13 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
         }
         // DEAD: back to the deepest level with an untried digit
         for (;;) {
-            if (depth == 0) return W_UNSOLVABLE;
+            if (depth == 0) {
+                if (mode == plane::M_COUNT && (mst & plane::MST_FOUND)) {  // exactly one completion
+                    w = stk.restore(sol_level, L);
+                    return W_SOLVED;
+                }
+                return W_UNSOLVABLE;
+            }
             depth--;
             const uint32_t e = stk.entry(depth);
             const uint32_t rem = (e >> 8) & 0x1FFu;

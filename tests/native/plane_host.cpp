@@ -20,6 +20,11 @@ static void words_of(const uint8_t *src, uint32_t (&x)[21])
                ((uint32_t)buf[4 * k + 3] << 24);
 }
 
+// the search-mode switch of plane::solve (0 = the walk only), for every
+// solve below
+static uint32_t g_mrv_after = 0;
+extern "C" void plane_set_mrv_after(uint32_t k) { g_mrv_after = k; }
+
 // status: 1 solved, 0 no completion, -1 invalid byte, 2 left to the wave
 // kernel (clashing givens or depth overflow)
 extern "C" void plane_solve_batch(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n, int node_order,
@@ -38,7 +43,7 @@ extern "C" void plane_solve_batch(const uint8_t *in, uint8_t *out, int32_t *stat
         if (!plane::load_words(B, x, clash)) { status[i] = -1; continue; }
         if (clash) { status[i] = 2; continue; }
         plane::Stats st = {0, 0};
-        const int r = plane::solve(B, stk, node_order, max_depth, st);
+        const int r = plane::solve(B, stk, node_order, max_depth, st, g_mrv_after);
         g += st.guesses;
         p += st.passes;
         if (r == 1) plane::store_values(B, [&](int c, uint32_t v) { dst[c] = (uint8_t)v; });
@@ -110,7 +115,7 @@ extern "C" void plane_solve_stats(const uint8_t *in, int64_t n, int node_order, 
         if (!plane::load_words(B, x, clash) || clash) continue;
         plane::Stats st = {0, 0};
         stk.max_depth = 0;
-        plane::solve(B, stk, node_order, 81, st);
+        plane::solve(B, stk, node_order, 81, st, g_mrv_after);
         passes[i] = (int32_t)st.passes;
         guesses[i] = (int32_t)st.guesses;
         depth[i] = (int32_t)stk.max_depth;
@@ -269,7 +274,7 @@ extern "C" void plane_board_passes(const uint8_t *in, int64_t n, int node_order,
         passes[i] = guesses[i] = 0;
         if (!plane::load_words(B, x, clash) || clash) continue;
         plane::Stats st = {0, 0};
-        plane::solve(B, stk, node_order, 81, st);
+        plane::solve(B, stk, node_order, 81, st, g_mrv_after);
         passes[i] = st.passes;
         guesses[i] = st.guesses;
     }

@@ -30,6 +30,18 @@ struct WStack {
     void put_entry(uint32_t level, uint32_t e) const { w[level * LEVEL_WORDS + plane::STACK_ENTRY] = e; }
 };
 
+// the search-mode switch (plane::search_step / wide::solve; 0 = the walk only)
+static uint32_t g_mrv_after = 0;
+extern "C" void wide_set_mrv_after(uint32_t k) { g_mrv_after = k; }
+
+static uint32_t stack_words[MAX_LEVELS * LEVEL_WORDS];
+// the same words as plane::WordStack's put / get
+struct LineStack {
+    void put(uint32_t level, int k, uint32_t v) { stack_words[level * LEVEL_WORDS + k] = v; }
+    uint32_t get(uint32_t level, int k) const { return stack_words[level * LEVEL_WORDS + k]; }
+};
+static LineStack lines;
+
 static void words_of(const uint8_t *src, uint32_t (&x)[21])
 {
     uint8_t buf[84] = {0};
@@ -69,7 +81,6 @@ extern "C" void wide_solve_batch(const uint8_t *in, uint8_t *out, int32_t *statu
                                  uint32_t max_depth, uint32_t lane_guesses, uint64_t *guesses, uint64_t *passes_lane,
                                  uint64_t *passes_wide)
 {
-    static uint32_t stack_words[MAX_LEVELS * LEVEL_WORDS];
     const WStack stk = {stack_words};
     const wide::Lanes L = wide::lanes();
     uint64_t g = 0, pl = 0, pw = 0;
@@ -83,45 +94,18 @@ extern "C" void wide_solve_batch(const uint8_t *in, uint8_t *out, int32_t *statu
         bool clash = false;
         if (!plane::load_words(B, x, clash)) { status[i] = -1; continue; }
         if (clash) { status[i] = 2; continue; }
-        // ---- lane phase (plane_kernel's loop body)
-        uint32_t depth = 0, lg = 0;
+        // ---- lane phase (plane_kernel's loop body: pass + plane::search_step)
+        uint32_t depth = 0, lg = 0, mst = 0;
         int done = -2;  // -2: hand off
+        const plane::WordStack<LineStack> ls = {lines};
         while (lg < lane_guesses) {
             uint32_t und[3];
             const int r = plane::pass(B, und);
             pl++;
-            if (r == plane::SOLVED) { done = 1; break; }
-            if (r == plane::OPEN) continue;
-            if (r == plane::STUCK) {
-                if (depth == max_depth) { done = -1; break; }
-                int band, pos;
-                plane::pick_cell(und, node_order, band, pos);
-                const uint32_t cand = plane::cell_cand(B, band, pos);
-                const uint32_t d = cand & (0u - cand);
-                for (int w = 0; w < 27; ++w) stack_words[depth * LEVEL_WORDS + w] = B.P[w / 3][w % 3];
-                stack_words[depth * LEVEL_WORDS + plane::STACK_ENTRY] = plane::make_entry(band, pos, cand ^ d);
-                depth++;
-                lg++;
-                plane::set_cell(B, band, pos, d);
-                continue;
-            }
-            bool found = false;
-            while (depth > 0) {
-                depth--;
-                const uint32_t e = stack_words[depth * LEVEL_WORDS + plane::STACK_ENTRY];
-                const uint32_t rem = (e >> 8) & 0x1FFu;
-                if (!rem) continue;
-                const uint32_t d = rem & (0u - rem);
-                for (int w = 0; w < 27; ++w) B.P[w / 3][w % 3] = stack_words[depth * LEVEL_WORDS + w];
-                B.Det[0] = B.Det[1] = B.Det[2] = 0;
-                stack_words[depth * LEVEL_WORDS + plane::STACK_ENTRY] = e & ~(d << 8);
-                depth++;
-                lg++;
-                plane::set_cell(B, (int)((e >> 5) & 3u), (int)(e & 31u), d);
-                found = true;
-                break;
-            }
-            if (!found) { done = 0; break; }
+            const int s = plane::search_step(B, und, r, depth, mst, ls, node_order, max_depth, g_mrv_after, lg);
+            if (s == plane::S_CONT) continue;
+            done = s == plane::S_SOLVED ? 1 : s == plane::S_NONE ? 0 : -1;
+            break;
         }
         g += lg;
         if (done == 1) {
@@ -134,7 +118,7 @@ extern "C" void wide_solve_batch(const uint8_t *in, uint8_t *out, int32_t *statu
         // ---- wide phase: same planes (Det dropped), same stack and depth
         wide::V w = to_wave(B, L);
         wide::Stats st = {0, 0, 0};
-        const int r = wide::solve(w, depth, stk, L, node_order, max_depth, st, [] { return false; });
+        const int r = wide::solve(w, depth, stk, L, node_order, max_depth, st, [] { return false; }, mst, g_mrv_after);
         g += st.guesses;
         pw += st.passes;
         if (r == wide::W_SOLVED) {

@@ -127,3 +127,18 @@ def test_plane_tuning_rejects_oversized_chunks():
         assert L.sdk_set_plane_tuning(-1, -1, -1, 0) == 0
     finally:
         L.sdk_set_plane_tuning(-1, -1, -1, -1)
+
+
+def test_plane_search_knob_range():
+    """sdk_set_plane_search: the previous setting back (-1 = default),
+    out-of-range values refused.  Host-side only."""
+    from sudoku_solver_distributed_amd import _lib
+    L = _lib.load()
+    try:
+        L.sdk_set_plane_search(-1)
+        assert L.sdk_set_plane_search(64) == -1
+        assert L.sdk_set_plane_search(0) == 64
+        assert L.sdk_set_plane_search(1 << 24) == -1
+        assert L.sdk_set_plane_search(-1) == 0
+    finally:
+        L.sdk_set_plane_search(-1)

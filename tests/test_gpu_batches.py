@@ -114,3 +114,64 @@ def test_solve_inflight_grouped(solver):
         solver.solve_inflight(steps, outs, sts, group=2, ordered=True)
     with pytest.raises(ValueError):
         solver.solve_batches(steps[:1] * 17, outs[:1] * 17, sts[:1] * 17)
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_search_mode_switch_same_results(solver, order):
+    """sdk_set_plane_search: boards still searching after k passes restart
+    from their root counting completions (plane::search_step).  Bytes and
+    statuses never depend on k -- walk only (0), every board counting from
+    its first pass (1), and thresholds in between -- on hard 17-clue boards,
+    generated boards with many completions (the count's second completion
+    sends them back to the walk), search-heavy boards, no-completion boards
+    (one wrong clue added to a unique board), invalid bytes and clashing
+    givens; in the lane loop, in the wave-wide tail (tail 40) and across
+    batches (sdk_solve_batches)."""
+    from sudoku_solver_distributed_amd.gen import generate_batch, hard17_batch, hard_search_batch
+    lib = solver.lib
+    rng = np.random.default_rng(21)
+    nosol = hard17_batch(3000, seed=22).numpy()
+    sols, _ = O.solve_unique_batch(nosol[:300])
+    for i in range(300):  # one wrong clue: no completion (it would complete the unique board)
+        c = rng.choice(np.nonzero(nosol[i] == 0)[0])
+        nosol[i, c] = 1 + (sols[i, c] + rng.integers(0, 8)) % 9
+    parts = [hard17_batch(30_000, seed=23), generate_batch(1000, 52, seed=24).cpu(),
+             hard_search_batch(8000, seed=25), torch.from_numpy(nosol)]
+    p = torch.cat(parts).cuda()
+    p[11, 5] = 13
+    p[40_000] = torch.tensor(b81(CLASH), dtype=torch.uint8)
+    try:
+        assert lib.sdk_set_plane_search(0) == -1
+        want = [t.clone() for t in solver.solve(p, order=order)]
+        torch.cuda.synchronize()
+        # the generated boards (many completions) against the literal walk
+        g0, g1 = 30_000, 31_000
+        w, ws = O.solve_batch(p[g0:g1].cpu().numpy(), order=order)
+        assert np.array_equal(want[0][g0:g1].cpu().numpy(), w) and np.array_equal(want[1][g0:g1].cpu().numpy(), ws)
+        for k in (1, 8, 48, 128):
+            assert lib.sdk_set_plane_search(k) >= 0
+            for tail in (8, 40):
+                assert lib.sdk_set_plane_tuning(-1, tail, -1, -1) == 0
+                got = solver.solve(p, order=order)
+                torch.cuda.synchronize()
+                assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]), (k, tail)
+        # across batches, and ordered mode (frontier split semantics)
+        assert lib.sdk_set_plane_search(1) >= 0
+        cut = [0, 7_000, 30_500, 36_000, p.shape[0]]
+        bs = [p[a:b] for a, b in zip(cut, cut[1:])]
+        outs = [torch.empty_like(b) for b in bs]
+        sts = [torch.empty(b.shape[0], dtype=torch.int32, device=b.device) for b in bs]
+        solver.solve_batches(bs, outs, sts, order=order, grid_waves=1)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs), want[0]) and torch.equal(torch.cat(sts), want[1])
+        h = hard17_batch(20_000, seed=26).cuda()
+        s1, t1 = solver.solve(h, ordered=True, order=order)
+        torch.cuda.synchronize()
+        t1 = t1.cpu().numpy()
+        assert t1[0] == 1 and set(np.unique(t1).tolist()) <= {1, -2}
+        done = np.nonzero(t1 == 1)[0][:256]
+        wu, cnt = O.solve_unique_batch(h[done].cpu().numpy())
+        assert np.array_equal(s1[done].cpu().numpy(), wu)
+    finally:
+        lib.sdk_set_plane_search(-1)
+        lib.sdk_set_plane_tuning(-1, -1, -1, -1)

@@ -26,7 +26,18 @@ def host(tmp_path_factory):
                                       ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
     lib.plane_check_load.argtypes = [ctypes.c_void_p, ctypes.c_int64]
     lib.plane_check_load.restype = ctypes.c_int64
+    lib.plane_set_mrv_after.argtypes = [ctypes.c_uint32]
+    lib.plane_set_mrv_after(0)
     return lib
+
+
+@pytest.fixture(params=[0, 1, 24, 128], ids=lambda k: f"mrv{k}")
+def mrv_after(request, host):
+    """plane::solve's search-mode switch (M_WALK -> M_COUNT after k passes,
+    0 = never): results never depend on it."""
+    host.plane_set_mrv_after(request.param)
+    yield request.param
+    host.plane_set_mrv_after(0)
 
 
 def _solve(lib, boards, node_order=0, max_depth=81, stats=None):
@@ -69,7 +80,7 @@ def test_plane_golden_solve_and_node(host):
 
 
 @pytest.mark.parametrize("order", ["gen", "node"])
-def test_plane_generated_vs_literal_walk(host, order):
+def test_plane_generated_vs_literal_walk(host, order, mrv_after):
     from sudoku_solver_distributed_amd.gen import hard17_batch
     # gen.py-style boards on the CPU: complete grids with 55 cells erased
     grids, _ = O.solve_unique_batch(hard17_batch(200, seed=4321).numpy())
@@ -89,7 +100,7 @@ def test_plane_generated_vs_literal_walk(host, order):
 
 
 @pytest.mark.parametrize("order", ["gen", "node"])
-def test_plane_hard17_vs_oracle(host, order):
+def test_plane_hard17_vs_oracle(host, order, mrv_after):
     from sudoku_solver_distributed_amd.gen import hard17_batch
     boards = hard17_batch(256, seed=7).numpy()
     stats = {}
@@ -99,6 +110,27 @@ def test_plane_hard17_vs_oracle(host, order):
     assert (st == 1).all()
     assert (out == want).all()
     print(order, "passes/board", stats["passes"] / len(boards), "guesses/board", stats["guesses"] / len(boards))
+
+
+@pytest.mark.parametrize("order", ["gen", "node"])
+def test_plane_count_mode_unsolvable_and_multi(host, order, mrv_after):
+    """Boards the completion count sees no completion on: 17-clue boards
+    with one more (wrong) clue -- no completion, or clashing givens left to
+    the wave kernel."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    rng = np.random.default_rng(11)
+    b = hard17_batch(300, seed=12).numpy()
+    sols, _ = O.solve_unique_batch(b)
+    for i in range(len(b)):
+        c = rng.choice(np.nonzero(b[i] == 0)[0])
+        b[i, c] = 1 + (sols[i, c] + rng.integers(0, 8)) % 9  # a digit the completion does not hold
+    out, st = _solve(host, b, node_order=int(order == "node"))
+    # no completion by construction: one would also complete the unique
+    # 17-clue board, whose completion does not hold the added digit
+    mine = st != 2
+    assert mine.sum() > 50 and (st[mine] == 0).all() and np.array_equal(out[mine], b[mine])
+    # (boards with many completions: test_plane_generated_vs_literal_walk,
+    # where at mrv1 every board starts counting and goes back to the walk)
 
 
 def test_plane_depth_overflow_defers(host):
@@ -154,6 +186,8 @@ def wide(tmp_path_factory):
                                      ctypes.c_void_p, ctypes.c_void_p]
     lib.wide_check_fixpoint.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
     lib.wide_check_fixpoint.restype = ctypes.c_int64
+    lib.wide_set_mrv_after.argtypes = [ctypes.c_uint32]
+    lib.wide_set_mrv_after(0)
     return lib
 
 
@@ -192,7 +226,7 @@ def test_wide_fixpoint_matches_lane_pass(wide):
 
 @pytest.mark.parametrize("order", ["gen", "node"])
 @pytest.mark.parametrize("lane_guesses", [0, 1, 3])
-def test_wide_continuation_vs_lane_solver(host, wide, order, lane_guesses):
+def test_wide_continuation_vs_lane_solver(host, wide, order, lane_guesses, mrv_after):
     """Hand a board from the lane solver to the wave-wide solver after
     `lane_guesses` guesses (0: the whole search wide): identical answers and
     statuses.  The wide pass eliminates this pass's hidden singles at once,
@@ -202,10 +236,16 @@ def test_wide_continuation_vs_lane_solver(host, wide, order, lane_guesses):
     no = int(order == "node")
     s_lane, s_wide = {}, {}
     want, wst = _solve(host, boards, node_order=no, stats=s_lane)
-    got, gst = _wide(wide, boards, node_order=no, lane_guesses=lane_guesses, stats=s_wide)
+    wide.wide_set_mrv_after(mrv_after)  # the board's search mode is handed over too
+    try:
+        got, gst = _wide(wide, boards, node_order=no, lane_guesses=lane_guesses, stats=s_wide)
+    finally:
+        wide.wide_set_mrv_after(0)
     assert np.array_equal(gst, wst)
     assert np.array_equal(got, want)
-    assert s_wide["guesses"] <= 1.01 * s_lane["guesses"]
+    # (the completion count walks whole subtrees, contradictory states
+    # included, where the two passes may part for a pass: a little more noise)
+    assert s_wide["guesses"] <= (1.01 if mrv_after == 0 else 1.05) * s_lane["guesses"]
     if lane_guesses == 0:
         assert s_wide["passes_wide"] > 0 and s_wide["passes_lane"] == 0
 
