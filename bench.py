@@ -368,6 +368,8 @@ def main():
     ap.add_argument("--mrv-after", type=int, default=-1,
                     help="passes on a board before its search switches to the completion count "
                          "(sdk_set_plane_search; -1: the library default, 0: the walk's order only) -- A/B only")
+    ap.add_argument("--no-serial", action="store_true",
+                    help="skip the back-to-back comparison (profiling runs: only the timed launch shape runs)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the configs[1] / configs[3] side measurements")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -479,7 +481,7 @@ def main():
 
     # the same steps back to back (one launch in flight), for comparison
     serial = None
-    if m > 1:
+    if m > 1 and not args.no_serial:
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()
         steps(args.steps, inflight=1)

@@ -197,7 +197,7 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk);
  * fewest-candidates cells: exactly one completion is the walk's answer, none
  * means none for the walk too, two send the board back to the walk's own
  * branch order.  0 keeps every board on the walk's order; -1
- * restores the default ($SDK_PLANE_MRV, built-in 128).  Results never
+ * restores the default ($SDK_PLANE_MRV, built-in 64).  Results never
  * depend on it.  Returns the previous setting (-1: default), -1 for an
  * out-of-range value (nothing changed). */
 int sdk_set_plane_search(int mrv_after);

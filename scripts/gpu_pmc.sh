@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 B=${BATCH:-1048576}
 W=${WORKLOAD:-hard17}
 # the bench's default launch shape (BENCH_EXTRA adds flags, e.g. --launch-boards)
-CMD="python -u bench.py --steps 6 --warmup 1 --batch $B --no-cpu --latency-boards 0 --no-extras --workload $W $BENCH_EXTRA"
+CMD="python -u bench.py --steps 6 --warmup 1 --batch $B --no-cpu --latency-boards 0 --no-extras --no-serial --workload $W $BENCH_EXTRA"
 run() {  # name counters...
   local name=$1; shift
   rm -rf gpurun_out/pmc_$name

@@ -29,12 +29,16 @@ def main():
     out, batch, seed, dirs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4:]
     kernel = os.environ.get("PMC_KERNEL", "")
     vals = defaultdict(list)
+    grids = set()
     for d in dirs:
         rows = [r for r in load(d) if r.get("Kernel_Name", "").split("(")[0] in
                 ((kernel,) if kernel else ("plane_kernel",))]
         if not rows:
             continue
+        # the bench runs only its timed launch shape under the profiler
+        # (--no-serial), the deferred-board kernel aside: one grid size
         gmax = max(int(r.get("Grid_Size", 0) or 0) for r in rows)
+        grids.add(gmax)
         per = defaultdict(float)
         for r in rows:
             if int(r.get("Grid_Size", 0) or 0) != gmax:
@@ -55,6 +59,7 @@ def main():
         except OSError:
             pass
     res = {"kernel": kernel or "plane_kernel", "batch": batch, "seed": seed, "shape": shape,
+           "grid_threads": sorted(grids),
            "workload": os.environ.get("PMC_WORKLOAD", "hard17"),
            "counters_per_launch": summary,
            "valu_insts_per_launch": summary.get("SQ_INSTS_VALU"),

@@ -55,7 +55,7 @@
 // passes on a board before its search switches from the walk's branch order
 // to the completion count (plane::search_step; 0: never)
 #ifndef SDK_PLANE_MRV
-#define SDK_PLANE_MRV 128
+#define SDK_PLANE_MRV 64
 #endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
