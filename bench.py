@@ -13,11 +13,12 @@ GPU per step.  A shard of a step too small to fill the GPU alone (2^17 boards
 at N = 8) is launched together with the rank's next steps' shards --
 sdk_solve_batches, one queue over up to 16 batches that drains once -- until a
 launch holds --launch-boards (2^20) boards; each step's shard keeps its own
-input and output buffers.  Consecutive launches keep --inflight (default 3)
-in flight per GPU, each on its own stream and workspace, each launch's grid
-holding --grid-waves (default 2) waves per SIMD (BatchSolver.solve_inflight):
-two launches are resident at once and a third fills the first one's drain;
-`serial` reports the same steps back to back on full grids.  value = all
+input and output buffers.  Consecutive launches keep --inflight (default 6,
+with $GPU_MAX_HW_QUEUES = 8 set below) in flight per GPU, each on its own
+stream and workspace, each launch's grid holding --grid-waves (default 1)
+wave per SIMD (BatchSolver.solve_inflight): four launches are resident at
+once and the next ones fill their drains as their waves exit; `serial`
+reports the same steps back to back on full grids.  value = all
 ranks' boards / max-over-ranks wall time.
 
 Rank 0 prints ONE JSON line with the contract fields plus:
@@ -46,6 +47,11 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# hardware queues per process (HIP's default is 4), read when HIP starts:
+# each launch in flight has its own stream, and streams past the queues
+# share one and serialise (six launches in flight need 8)
+if not os.environ.get("GPU_MAX_HW_QUEUES", "").isdigit() or int(os.environ["GPU_MAX_HW_QUEUES"]) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"  # (the GPU boxes export HIP's default, 4)
 
 PEAK_VALU_OPS = 256 * 4 * 32 * 2.4e9   # lane-ops/s: 256 CU x 4 SIMD32 x 2.4 GHz
 PEAK_HBM = 8.0e12                       # B/s (MI355X_MICROARCH.md)
@@ -231,9 +237,10 @@ def e2e_rate(solver, boards, reps: int = 3):
 def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
     """configs[2]'s per-GPU regime under strong scaling, on one GPU: steps of
     B/2, B/4, B/8 boards (a rank's shard of the B-board step at N = 2, 4, 8),
-    three launches in flight, either one step per launch (`ungrouped`) or
+    either one step per launch (`ungrouped`) or
     consecutive steps' shards in one sdk_solve_batches launch of
-    `launch_boards` boards (`grouped`, the bench's strong-scaling steps).
+    `launch_boards` boards (`grouped`, the bench's strong-scaling steps);
+    launches in flight as the bench's (solver.default_inflight).
     8 B boards per measurement, best of `reps`; every step checked SOLVED."""
     import torch
     n = boards.shape[0]
@@ -243,14 +250,16 @@ def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
         parts = [boards[j * sh:(j + 1) * sh] for j in range(div)]
         k = 8 * div
         res = {"boards_per_step": sh, "steps": k}
+        from sudoku_solver_distributed_amd.solver import default_inflight
+        m = default_inflight()[0]
         for name, g in (("ungrouped", 1), ("grouped", max(1, min(16, -(-launch_boards // sh))))):
-            nb = 3 * max(g, div)
+            nb = m * max(g, div)
             bufs = [(torch.empty_like(parts[0]), torch.empty(sh, dtype=torch.int32, device=boards.device))
                     for _ in range(nb)]
 
             def run(kk):
                 solver.solve_inflight([parts[i % div] for i in range(kk)], [bufs[i % nb][0] for i in range(kk)],
-                                      [bufs[i % nb][1] for i in range(kk)], inflight=3, group=g)
+                                      [bufs[i % nb][1] for i in range(kk)], inflight=m, group=g)
             run(2 * g)
             best = None
             for _ in range(reps):
@@ -266,7 +275,7 @@ def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
     return out
 
 
-def side_configs(solver, dev, world, rank, boards):
+def side_configs(solver, dev, world, rank, boards, serving: bool = True):
     """BASELINE.json configs[1], [2]'s per-GPU shard regime, [3] and [4], a
     search-heavy batch and the PCIe-inclusive rate, outside the timed region.
 
@@ -304,7 +313,9 @@ def side_configs(solver, dev, world, rank, boards):
                               "passes_per_board": s3["sweeps"] / max(s3["finished"], 1),
                               "deferred_per_call": s3["deferred"] / 3, "all_solved_and_checked": ok}
         # the same batch as steps with launches in flight (the headline's method)
-        k, m = 9, 3
+        from sudoku_solver_distributed_amd.solver import default_inflight
+        m = default_inflight()[0]
+        k = 3 * m
         hb = [(torch.empty_like(hs), torch.empty(hs.shape[0], dtype=torch.int32, device=dev)) for _ in range(m)]
         solver.solve_inflight([hs] * m, [b[0] for b in hb], [b[1] for b in hb], inflight=m)
         torch.cuda.synchronize()
@@ -315,6 +326,7 @@ def side_configs(solver, dev, world, rank, boards):
         out["hard_search"]["inflight"] = {"steps": k, "boards_per_s": hs.shape[0] / ti,
                                           "identical": all(bool(torch.equal(b[0], sols)) for b in hb)}
         out["e2e"] = e2e_rate(solver, boards)
+    if rank == 0 and serving:
         # configs[4]: peers in THIS process (GIL-bound, labelled so) and
         # peers as their own node.py processes (the reference's shape)
         out["node_http"] = node_load(dev)
@@ -357,12 +369,13 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--latency-boards", type=int, default=32,
                     help="boards timed one per launch for p50_single_ms (0 = skip; profiling runs)")
-    ap.add_argument("--inflight", type=int, default=3,
+    ap.add_argument("--inflight", type=int, default=-1,
                     help="launches in flight per GPU (BatchSolver.solve_inflight: each on its own stream and "
-                         "workspace, so one launch's drain overlaps the next ones); 1 = back to back")
+                         "workspace, so one launch's drain overlaps the next ones); 1 = back to back; "
+                         "-1: solver.default_inflight() (6 with >= 8 hardware queues, else 3)")
     ap.add_argument("--grid-waves", type=int, default=-1,
-                    help="waves per SIMD in each launch's grid (sdk_solve_batch_grid; -1: solve_inflight's "
-                         "default, 2 with launches in flight, a full grid at --inflight 1; 0: a full grid)")
+                    help="waves per SIMD in each launch's grid (sdk_solve_batch_grid; -1: the default for the "
+                         "launches in flight, a full grid at --inflight 1; 0: a full grid)")
     ap.add_argument("--launch-events", action="store_true",
                     help="also time each launch's own span with events on its slot stream (launch_ms)")
     ap.add_argument("--mrv-after", type=int, default=-1,
@@ -370,6 +383,8 @@ def main():
                          "(sdk_set_plane_search; -1: the library default, 0: the walk's order only) -- A/B only")
     ap.add_argument("--no-serial", action="store_true",
                     help="skip the back-to-back comparison (profiling runs: only the timed launch shape runs)")
+    ap.add_argument("--no-serving", action="store_true",
+                    help="skip the configs[4] HTTP serving figures (peers in this process and as processes)")
     ap.add_argument("--no-extras", action="store_true",
                     help="skip the configs[1] / configs[3] side measurements")
     ap.add_argument("--dist-backend", choices=("nccl", "gloo"), default="nccl",
@@ -425,7 +440,9 @@ def main():
         inputs.append(full[lo:hi].contiguous().to(dev))
         del full
     boards = inputs[0]
-    m = max(1, args.inflight)
+    from sudoku_solver_distributed_amd.solver import default_inflight
+    m_def, gw_def = default_inflight()
+    m = m_def if args.inflight < 0 else max(1, args.inflight)
     # one (solutions, status) pair per step that can be in flight: step i
     # reads inputs[i % group] and writes pair i % (m * group)
     nb = m * group
@@ -433,12 +450,13 @@ def main():
     out, status = bufs[0]
     stream = torch.cuda.current_stream(dev)
     solver._slot_solvers(m)  # slot workspaces allocated before any timing
-    grid_waves = None if args.grid_waves < 0 else args.grid_waves
-    if grid_waves is None:
-        from sudoku_solver_distributed_amd.solver import GRID_WAVES_INFLIGHT
-        grid_waves_used = GRID_WAVES_INFLIGHT if m > 1 else 0
+    if args.grid_waves >= 0:
+        grid_waves = args.grid_waves
+    elif m == 1:
+        grid_waves = 0
     else:
-        grid_waves_used = grid_waves
+        grid_waves = gw_def if args.inflight < 0 else (1 if m >= 5 else 2)
+    grid_waves_used = grid_waves
 
     def steps(k, events=None, inflight=m):
         solver.solve_inflight([inputs[i % group] for i in range(k)], [bufs[i % nb][0] for i in range(k)],
@@ -501,7 +519,7 @@ def main():
     lat.sort()
     p50 = lat[len(lat) // 2] if lat else None
 
-    extras = None if args.no_extras else side_configs(solver, dev, world, rank, boards)
+    extras = None if args.no_extras else side_configs(solver, dev, world, rank, boards, serving=not args.no_serving)
 
     if rank != 0:
         if world > 1:

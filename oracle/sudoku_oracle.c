@@ -350,6 +350,106 @@ void oracle_solve_unique_batch(const uint8_t *in, uint8_t *out, int32_t *count, 
     for (int64_t p = 0; p < n; p++) count[p] = oracle_solve_unique(in + p * 81, out + p * 81);
 }
 
+/* Test helper: the same count (to 2, first completion kept) with naked and
+ * hidden singles propagated before each branch on a fewest-candidates cell.
+ * Propagation only removes candidates no completion can use, so the
+ * completions and their count are the plain search's (checked against
+ * oracle_solve_unique in tests/test_oracle.py); hard 17-clue boards need
+ * ~100x fewer nodes.  Givens that clash count 0 here where the plain
+ * search (which never tests givens) may find fills: callers use it only on
+ * boards whose givens do not clash. */
+static int prop_singles(uint16_t *c)
+{
+    static const int U[27][9] = {
+#define R(r) {9 * r, 9 * r + 1, 9 * r + 2, 9 * r + 3, 9 * r + 4, 9 * r + 5, 9 * r + 6, 9 * r + 7, 9 * r + 8}
+        R(0), R(1), R(2), R(3), R(4), R(5), R(6), R(7), R(8),
+#undef R
+#define C(k) {k, 9 + k, 18 + k, 27 + k, 36 + k, 45 + k, 54 + k, 63 + k, 72 + k}
+        C(0), C(1), C(2), C(3), C(4), C(5), C(6), C(7), C(8),
+#undef C
+#define B(b) {27 * (b / 3) + 3 * (b % 3), 27 * (b / 3) + 3 * (b % 3) + 1, 27 * (b / 3) + 3 * (b % 3) + 2, \
+              27 * (b / 3) + 3 * (b % 3) + 9, 27 * (b / 3) + 3 * (b % 3) + 10, 27 * (b / 3) + 3 * (b % 3) + 11, \
+              27 * (b / 3) + 3 * (b % 3) + 18, 27 * (b / 3) + 3 * (b % 3) + 19, 27 * (b / 3) + 3 * (b % 3) + 20}
+        B(0), B(1), B(2), B(3), B(4), B(5), B(6), B(7), B(8),
+#undef B
+    };
+    for (int changed = 1; changed;) {
+        changed = 0;
+        for (int i = 0; i < 81; i++) {
+            if (!c[i]) return 0;
+            if (c[i] & (c[i] - 1)) continue;
+            const int r = i / 9, col = i % 9, b = (r / 3) * 3 + col / 3;
+            const int *us[3] = {U[r], U[9 + col], U[18 + b]};
+            for (int u = 0; u < 3; u++)
+                for (int k = 0; k < 9; k++) {
+                    const int p = us[u][k];
+                    if (p != i && (c[p] & c[i])) {
+                        c[p] &= (uint16_t)~c[i];
+                        if (!c[p]) return 0;
+                        changed = 1;
+                    }
+                }
+        }
+        for (int u = 0; u < 27; u++) {
+            uint16_t once = 0, twice = 0;
+            for (int k = 0; k < 9; k++) {
+                twice |= once & c[U[u][k]];
+                once |= c[U[u][k]];
+            }
+            if (once != 0x1FF) return 0;
+            const uint16_t single = once & (uint16_t)~twice;
+            for (int k = 0; single && k < 9; k++) {
+                const int p = U[u][k];
+                const uint16_t x = c[p] & single;
+                if (x && c[p] != x) {
+                    if (x & (x - 1)) return 0;
+                    c[p] = x;
+                    changed = 1;
+                }
+            }
+        }
+    }
+    return 1;
+}
+
+static int uniqp_rec(uint16_t *c, int *count, uint8_t *first)
+{
+    if (!prop_singles(c)) return 0;
+    int best = -1, bn = 10;
+    for (int i = 0; i < 81; i++) {
+        const int n = __builtin_popcount(c[i]);
+        if (n > 1 && n < bn) { bn = n; best = i; if (n == 2) break; }
+    }
+    if (best < 0) {
+        if (*count == 0)
+            for (int i = 0; i < 81; i++) first[i] = (uint8_t)(__builtin_ctz(c[i]) + 1);
+        (*count)++;
+        return *count >= 2;
+    }
+    for (uint16_t m = c[best]; m; m &= (uint16_t)(m - 1)) {
+        uint16_t s[81];
+        memcpy(s, c, sizeof s);
+        s[best] = m & (uint16_t)(0u - m);
+        if (uniqp_rec(s, count, first)) return 1;
+    }
+    return 0;
+}
+
+int oracle_solve_unique_prop(const uint8_t *g_in, uint8_t *out)
+{
+    uint16_t c[81];
+    memcpy(out, g_in, 81);
+    for (int i = 0; i < 81; i++) c[i] = g_in[i] ? (uint16_t)(1u << (g_in[i] - 1)) : 0x1FF;
+    int count = 0;
+    uniqp_rec(c, &count, out);
+    return count;
+}
+
+void oracle_solve_unique_prop_batch(const uint8_t *in, uint8_t *out, int32_t *count, int64_t n)
+{
+    for (int64_t p = 0; p < n; p++) count[p] = oracle_solve_unique_prop(in + p * 81, out + p * 81);
+}
+
 /* Timed batch walk for bench.py's cpu_baseline: solves boards in order until
  * `seconds` of wall time have elapsed; returns the number of boards fully
  * solved (a board cut off by the deadline is not counted). */

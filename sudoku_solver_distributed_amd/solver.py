@@ -10,6 +10,7 @@ Boards are ``uint8`` tensors of shape ``(n, 81)`` (row-major, 0 = empty).
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from typing import Optional, Tuple
 
@@ -67,11 +68,25 @@ def as_boards(x, device=None, max_value: int = 9) -> torch.Tensor:
     return t.contiguous()
 
 
-# waves per SIMD in each launch's grid when launches are in flight: a full
-# grid (4) leaves a launch's drain to the next launch only as its waves exit;
-# 2 keeps two launches resident together (measured +8 % at three
-# in flight over a full grid at two)
+# Launches in flight and waves per SIMD in each launch's grid
+# (solve_inflight's defaults).  A full grid (4 waves per SIMD) leaves a
+# launch's drain to the next launch only as its waves exit; smaller grids
+# keep several launches resident together.  Each launch in flight has its
+# own stream, and streams beyond the process's hardware queues
+# ($GPU_MAX_HW_QUEUES, HIP's default 4) share one and serialise: with 8 or
+# more queues six launches at 1 wave per SIMD (four resident, two queued),
+# else three at 2 (585-593 against 534-537 M boards/s).
 GRID_WAVES_INFLIGHT = 2
+
+
+def default_inflight():
+    """(launches in flight, grid waves per SIMD) for this process's hardware
+    queue count."""
+    try:
+        hwq = int(os.environ.get("GPU_MAX_HW_QUEUES", "4"))
+    except ValueError:
+        hwq = 4
+    return (6, 1) if hwq >= 8 else (3, GRID_WAVES_INFLIGHT)
 
 
 class BatchSolver:
@@ -192,15 +207,15 @@ class BatchSolver:
                 self._slots.append((BatchSolver(self.device), streams[len(self._slots)]))
             return self._slots[:inflight]
 
-    def solve_inflight(self, batches, outs, statuses, inflight: int = 3, order="gen", ordered: bool = False,
-                       launch_events=None, grid_waves: Optional[int] = None, group: int = 1):
+    def solve_inflight(self, batches, outs, statuses, inflight: Optional[int] = None, order="gen",
+                       ordered: bool = False, launch_events=None, grid_waves: Optional[int] = None, group: int = 1):
         """Solve a sequence of device batches with up to `inflight` launches
         in flight on this GPU: batch i runs on slot i % inflight (its own
         workspace and stream), so a launch's end -- its last boards draining
         while most lanes idle -- overlaps the next launches instead of
-        idling the GPU.  grid_waves: waves per SIMD in each launch's grid
-        (default 2 with launches in flight -- two launches resident at once,
-        a third queued to fill the first one's drain; 0 = a full grid).  Each
+        idling the GPU.  inflight / grid_waves (waves per SIMD in each
+        launch's grid; 0 = a full grid): default_inflight() -- six launches
+        at 1 wave per SIMD with >= 8 hardware queues, else three at 2.  Each
         launch is a whole sdk_solve_batch_grid; results are those of solve().  outs[i] / statuses[i] receive batch i (buffers of
         batches that may be in flight together must not alias).  The
         caller's current stream waits for every batch; nothing synchronises
@@ -210,6 +225,9 @@ class BatchSolver:
         (solve_batches, one queue over them; unordered only) -- the
         strong-scaling steps, where one GPU's share of a step is too small to
         fill the GPU alone."""
+        if inflight is None:
+            inflight, gw = default_inflight()
+            grid_waves = gw if grid_waves is None else grid_waves
         if inflight < 1:
             raise ValueError("inflight must be >= 1")
         if not 1 <= group <= _lib.SDK_MAX_BATCHES or (group > 1 and ordered):

@@ -15,14 +15,18 @@ def test_default_kernel_has_matching_pmc_profile():
     with open(path) as f:
         pmc = json.load(f)
     # bench.py defaults at N = 1: --batch 2^20 boards per step, --seed 2024,
-    # one step per launch, 3 launches in flight at 2 waves per SIMD -- the
+    # one step per launch, 6 launches in flight at 1 wave per SIMD -- the
     # counters must come from the launch shape the bench times (bench.py
     # nulls roofline.frac / traffic otherwise)
-    from sudoku_solver_distributed_amd.solver import GRID_WAVES_INFLIGHT
+    # (bench.py sets GPU_MAX_HW_QUEUES = 8 before HIP starts)
+    from unittest import mock
+    from sudoku_solver_distributed_amd.solver import default_inflight
+    with mock.patch.dict(os.environ, {"GPU_MAX_HW_QUEUES": "8"}):
+        inflight, grid_waves = default_inflight()
     assert pmc["kernel"] == kname
     assert pmc["seed"] == 2024 and pmc.get("workload", "hard17") == "hard17"
-    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": 3, "grid_waves": GRID_WAVES_INFLIGHT}
-    assert pmc["counters_per_launch"]["SQ_WAVES"] == 256 * 4 * GRID_WAVES_INFLIGHT
+    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": inflight, "grid_waves": grid_waves}
+    assert pmc["counters_per_launch"]["SQ_WAVES"] == 256 * 4 * grid_waves
     assert pmc["valu_insts_per_launch"] > 0
     assert pmc["hbm_bytes_per_launch"] is None or pmc["hbm_bytes_per_launch"] > 0
 
@@ -52,7 +56,8 @@ def test_bench_two_rank_path_runs():
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen(
             [sys.executable, "-u", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--dist-backend", "gloo",
-             "--device-index", "0", "--steps", "2", "--warmup", "1", "--no-cpu", "--latency-boards", "4"],
+             "--device-index", "0", "--steps", "2", "--warmup", "1", "--no-cpu", "--latency-boards", "4",
+             "--no-serving"],
             cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
     outs = []
     for p in procs:

@@ -356,13 +356,19 @@ def test_stats_agree_between_kernels(solver):
     plane kernel's per-lane counters are summed over the wave).  The plane
     pass notices two equal determined cells in one unit only some passes
     later (plane_solver.h), so it may branch inside an already-dead node the
-    wave kernel prunes: plane >= packed, by a hair."""
+    wave kernel prunes: plane >= packed, by a few % (with the walk's order
+    only, sdk_set_plane_search(0)).  The default search-mode switch needs
+    fewer."""
     from sudoku_solver_distributed_amd import _lib
     from sudoku_solver_distributed_amd.gen import hard17_batch
     p = hard17_batch(20000, seed=3).to(solver.device)
     got = {}
-    for kernel in ("packed", "plane"):
-        prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel])
+    for kernel in ("packed", "plane", "plane_count"):
+        prev = solver.lib.sdk_set_solve_kernel(_lib.SDK_KERNELS[kernel.split("_")[0]])
+        # the walk's own branch order for the like-for-like count; then the
+        # default search-mode switch (heavy boards count completions on
+        # fewest-candidates cells: fewer guesses)
+        solver.lib.sdk_set_plane_search(-1 if kernel == "plane_count" else 0)
         try:
             solver.stats(reset=True)
             sols, st = solver.solve(p)
@@ -371,12 +377,16 @@ def test_stats_agree_between_kernels(solver):
             assert bool((st == 1).all())
         finally:
             solver.lib.sdk_set_solve_kernel(prev)
-    for k in ("packed", "plane"):
+            solver.lib.sdk_set_plane_search(-1)
+    for k in ("packed", "plane", "plane_count"):
         assert got[k]["finished"] == 20000 and got[k]["solved"] == 20000, got
+    assert got["plane_count"]["guesses"] < got["plane"]["guesses"], got
     # the plane kernel hands the last boards of sparse waves to the wave kernel
     assert got["packed"]["deferred"] == 0 and got["plane"]["deferred"] < 20000, got
     assert got["packed"]["guesses"] > 20000 * 0.3, got
-    assert got["packed"]["guesses"] <= got["plane"]["guesses"] <= got["packed"]["guesses"] * 1.01 + 16, got
+    # (six-seed corpus: within 1 %; the 80-class corpus searches ~20x more,
+    # and the lazily noticed duplicate digits cost ~9 % more branch nodes)
+    assert got["packed"]["guesses"] <= got["plane"]["guesses"] <= got["packed"]["guesses"] * 1.15 + 16, got
     assert got["plane"]["sweeps"] > 20000 * 5, got
 
 
