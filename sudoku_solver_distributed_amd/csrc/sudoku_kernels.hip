@@ -502,6 +502,9 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
 }
 static std::atomic<int> g_bpc_packed{0}, g_bpc_plane{0};
 
+// waves of the deferred-board kernels after a plane launch
+static int64_t deferred_waves() { return (int64_t)cu_count(); }
+
 // lanes of a full plane-kernel grid on the current device, and the bytes of
 // their stacks (the workspace holds them after WS_STACK_BYTE)
 static int64_t plane_max_threads()
@@ -617,8 +620,11 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
         int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
         e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, list, ordered, order, threads, st);
         if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
-        // the boards it left (clashing givens, deep searches): wave per board
-        const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_deferred_kernel, g_bpc_packed) * WAVES_PER_BLOCK;
+        // the boards it left (clashing givens, deep searches): wave per board,
+        // one wave per CU (its waves exit at once when nothing was left, and
+        // a full grid of them only queues for the slots the next launches in
+        // flight want)
+        const int64_t max_waves = deferred_waves();
         const int64_t groups = (n + 63) / 64;
         const int64_t waves = groups < max_waves ? groups : max_waves;
         hipLaunchKernelGGL(solvep_deferred_kernel, dim3((unsigned)((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
@@ -677,7 +683,7 @@ int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutio
     int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
     hipError_t e = sdk_launch_plane_multi(bs, ws, stack, list, order, threads, st);
     if (e != hipSuccess) return set_err("sdk_solve_batches: plane launch", e);
-    const int64_t max_waves = (int64_t)cu_count() * blocks_per_cu(solvep_deferred_multi_kernel, g_bpc_packed) * WAVES_PER_BLOCK;
+    const int64_t max_waves = deferred_waves();
     const int64_t groups = (total + 63) / 64;
     const int64_t waves = groups < max_waves ? groups : max_waves;
     hipLaunchKernelGGL(solvep_deferred_multi_kernel, dim3((unsigned)((waves + WAVES_PER_BLOCK - 1) / WAVES_PER_BLOCK)),
