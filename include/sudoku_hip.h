@@ -183,8 +183,9 @@ int sdk_set_solve_kernel(int kernel);
  * defaults are the measured optimum).  refill: idle lanes
  * before a wave refills; tail: active lanes at or below which a drained wave
  * hands its last boards to the tail solver (0 off, at most 40); tail_mode: 1
- * the wave-wide solver continues each search, 0 the wave-per-board solver
- * restarts it; chunk: most boards a wave claims from the queue at once (at
+ * the wave-wide solver continues each search, 2 the same through a per-XCD
+ * pool that every exiting wave of the XCD drains, 0 the wave-per-board
+ * solver restarts it; chunk: most boards a wave claims from the queue at once (at
  * most 64: a claim is staged and converted in one go; 0 one claim per refill).  A
  * negative value keeps that knob; all four negative restore the defaults
  * ($SDK_PLANE_REFILL / _TAIL / _TAIL_MODE / _CHUNK).  Results never depend on

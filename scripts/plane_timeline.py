@@ -25,9 +25,16 @@ for _ in range(3):
     solver.solve(boards)
 torch.cuda.synchronize()
 ws = solver.workspace
+ws[24 * 8:30 * 8].zero_()
+solver.solve(boards)
+torch.cuda.synchronize()
+pd = ws[24 * 8:30 * 8].view(torch.int64).cpu().numpy()
+if pd[0] or pd[1]:
+    print(f"tail pool: {pd[0]} claims, {pd[1]} failed claims, {pd[2]} flag polls; kcycles claiming {pd[3] / 1e3:.0f}, waiting {pd[4] / 1e3:.0f}, solving {pd[5] / 1e3:.0f}")
 cap = 1 << 20
 total = int(lib.sdk_workspace_bytes())
-list_off = total - cap * 8
+pool_bytes = 8 * (32 + 8192 * 37) * 4  # PLANE_POOL_BYTES (common.h), after the deferred list
+list_off = total - pool_bytes - cap * 8
 waves = (min(n, 256 * 4 * 256)) // 64
 st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 128].view(torch.int64).cpu().numpy().reshape(-1, 16)
 t0 = st[:, 0].min()

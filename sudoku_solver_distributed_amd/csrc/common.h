@@ -107,5 +107,17 @@ int sdk_plane_blocks_per_cu();
 // board indices the plane kernel hands to the wave kernel (int64 each; more
 // than this and the wave kernel finds them by scanning the statuses)
 #define PLANE_DEFER_CAP (1 << 20)
+// The drained waves' tail pool (plane_kernel.h, tail mode 2), after the
+// deferred list: per XCD, a 128-byte control line (reserved / published /
+// taken counts, re-armed every call), PLANE_POOL_CAP records of
+// PLANE_POOL_REC dwords, then one ready flag (uint32) per record.  A
+// consumer clears the flag it read, so the flags are zero again at the end
+// of every launch.
+#define PLANE_POOL_XCDS 8
+#define PLANE_POOL_CAP 8192
+#define PLANE_POOL_REC 36
+#define PLANE_POOL_CTL 32
+#define PLANE_POOL_STRIDE (PLANE_POOL_CTL + PLANE_POOL_CAP * (PLANE_POOL_REC + 1))  // dwords per XCD
+#define PLANE_POOL_BYTES ((size_t)PLANE_POOL_XCDS * PLANE_POOL_STRIDE * 4)
 
 #endif  // SDK_COMMON_H

@@ -44,10 +44,12 @@
 #define SDK_PLANE_REFILL 3
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 8
+#define SDK_PLANE_TAIL 16  // with the pool; 8 without (tail mode 1)
 #endif
+// 2: continue on the wave-wide solver through the XCD's tail pool, 1: the
+// same on the wave's own boards only, 0: restart on the wave-per-board solver
 #ifndef SDK_PLANE_TAIL_MODE
-#define SDK_PLANE_TAIL_MODE 1  // 1: continue on the wave-wide solver, 0: restart on the wave-per-board solver
+#define SDK_PLANE_TAIL_MODE 2
 #endif
 #ifndef SDK_PLANE_CHUNK
 #define SDK_PLANE_CHUNK 64
@@ -594,6 +596,143 @@ __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int
     st[3] = deferred;
 }
 
+// ---- the tail pool (tail mode 2; layout in common.h)
+// A drained wave's last boards go, as records in the tail record layout, to
+// its XCD's pool instead of its own LDS; every wave of the XCD takes records
+// from the pool, one at a time, before it exits.  Without it a wave finishes
+// its 8 tail boards one after another on the wide solver while the waves
+// around it have exited: the launch's end is one wave's serial tail.  One
+// pool per XCD so that producer and consumer share an L2: the records and
+// the donated stack lines are read back from that L2, and publishing them
+// takes no L2 writeback, only the producer's own store completions (vmcnt)
+// before the ready flag.
+//
+// Claims never retry on a shared word: a consumer takes one of the
+// PUBLISHED records by decrementing `avail` (and puts the unit back if the
+// count was already used up, then looks again), and only then draws its
+// slot from `head` with a fetch-add -- a slot below the published count, so
+// one a producer has reserved and is writing or has written.  (A
+// compare-and-swap on the head, 128 waves per XCD racing, measured 66 failed
+// swaps per record and a 25x slower launch.)
+#ifndef SDK_PLANE_POOL_INV
+#define SDK_PLANE_POOL_INV 1
+#endif
+struct PlanePool {
+    uint32_t *reserved;  // slots handed to producers (may pass PLANE_POOL_CAP: those boards stay local)
+    int32_t *avail;      // published records not yet taken (may dip below 0 while a claim backs out)
+    uint32_t *head;      // slots taken
+    uint32_t *recs;      // PLANE_POOL_CAP records of PLANE_POOL_REC dwords
+    uint32_t *flags;     // 1: the record is written
+};
+
+__device__ __forceinline__ PlanePool plane_pool(int64_t *defer_list)
+{
+    // the XCD this wave runs on (HW_REG_XCC_ID, bits 0..3)
+    const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & (PLANE_POOL_XCDS - 1);
+    uint32_t *base = (uint32_t *)(defer_list + PLANE_DEFER_CAP) + (size_t)x * PLANE_POOL_STRIDE;
+    uint32_t *recs = base + PLANE_POOL_CTL;
+    return {base, (int32_t *)(base + 1), base + 2, recs, recs + (size_t)PLANE_POOL_CAP * PLANE_POOL_REC};
+}
+
+// Take records from the pool until it is empty (wave-uniform).  A taken slot
+// has a producer that reserved it and writes it without waiting on anything,
+// so the flag wait is short; it is bounded all the same (~1 s) and a wave
+// that gives up leaves the pool.
+template <class IO>
+__device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t *stage, int lane,
+                                              __amdgpu_buffer_rsrc_t stack_rsrc, const IO &io,
+                                              unsigned long long *__restrict__ ws, int64_t *__restrict__ defer_list,
+                                              const int64_t *best, int node_order, uint32_t mrv_after,
+                                              uint32_t (&st)[5])
+{
+#if SDK_PLANE_STAMPS
+    // diagnostic: claims, backed-out claims, flag polls; cycles claiming, waiting, solving (ws words 24..29)
+    uint64_t d_ok = 0, d_fail = 0, d_poll = 0, c_claim = 0, c_wait = 0, c_solve = 0;
+    uint64_t d_t = __builtin_amdgcn_s_memtime();
+#endif
+    for (;;) {
+        int32_t a = 0;
+        if (lane == 0) a = __hip_atomic_load(pool.avail, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_readfirstlane(a) <= 0) break;
+        uint32_t h = 0;
+        if (lane == 0) {
+            a = __hip_atomic_fetch_add(pool.avail, -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (a > 0)
+                h = __hip_atomic_fetch_add(pool.head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            else
+                __hip_atomic_fetch_add(pool.avail, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        if (__builtin_amdgcn_readfirstlane(a) <= 0) {
+#if SDK_PLANE_STAMPS
+            d_fail++;
+#endif
+            continue;  // another wave took the last one: look again
+        }
+        h = __builtin_amdgcn_readfirstlane(h);
+#if SDK_PLANE_STAMPS
+        d_ok++;
+        {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            c_claim += t1 - d_t;
+            d_t = t1;
+        }
+#endif
+        uint32_t f = 0;
+        for (uint32_t tries = 0; tries < (1u << 23); ++tries) {
+            if (lane == 0) f = __hip_atomic_load(pool.flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            f = __builtin_amdgcn_readfirstlane(f);
+#if SDK_PLANE_STAMPS
+            d_poll++;
+#endif
+            if (f) break;
+            __builtin_amdgcn_s_sleep(2);
+        }
+        if (!f) break;
+#if SDK_PLANE_STAMPS
+        {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            c_wait += t1 - d_t;
+            d_t = t1;
+        }
+#endif
+#if SDK_PLANE_POOL_INV == 2
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+#elif SDK_PLANE_POOL_INV == 1
+        asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1 only
+#endif
+        const uint32_t *rec = pool.recs + (size_t)h * PLANE_POOL_REC;
+        const uint32_t w = lane < PLANE_TAIL_REC ? __hip_atomic_load(rec + lane, __ATOMIC_RELAXED,
+                                                                     __HIP_MEMORY_SCOPE_AGENT)
+                                                 : 0u;
+        if (lane < PLANE_TAIL_REC) stage[lane] = w;
+        if (lane == 0) __hip_atomic_store(pool.flags + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        wave_lds_sync();
+        uint32_t wst[5];
+        plane_wide_tail(stage, 1, lane, stack_rsrc, io, ws, defer_list, best, node_order, mrv_after, wst);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st[i] += wst[i];
+        wave_lds_sync();  // the record is read before the next one overwrites it
+#if SDK_PLANE_STAMPS
+        {
+            const uint64_t t1 = __builtin_amdgcn_s_memtime();
+            c_solve += t1 - d_t;
+            d_t = t1;
+        }
+#endif
+    }
+#if SDK_PLANE_STAMPS
+    c_claim += __builtin_amdgcn_s_memtime() - d_t;
+    if (lane == 0) {
+        atomicAdd(&ws[24], (unsigned long long)d_ok);
+        atomicAdd(&ws[25], (unsigned long long)d_fail);
+        atomicAdd(&ws[26], (unsigned long long)d_poll);
+        atomicAdd(&ws[27], (unsigned long long)c_claim);
+        atomicAdd(&ws[28], (unsigned long long)c_wait);
+        atomicAdd(&ws[29], (unsigned long long)c_solve);
+    }
+#endif
+}
+
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -1072,27 +1211,59 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     const uint32_t st_tailn = (uint32_t)__builtin_popcountll(tail_act);
     uint32_t st_tailp = 0;
 #endif
+    // tail mode 2: the tail boards go to this XCD's pool, which every wave
+    // of the XCD drains before it exits (plane_pool_drain)
+    const PlanePool pool = plane_pool(defer_list);
     if (tail_act && tail_mode) {
         // ---- wave-wide tail: the lanes' boards go to LDS records (27 plane
         // words, index, depth, stack line, guesses; stride 33 dwords, so the
         // lanes' writes and a record's reads are conflict-free) and the wave
         // continues each search in turn on the wide solver
         __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // the lanes' stack pushes have landed
+        const uint32_t k = (uint32_t)__builtin_popcountll(tail_act);
+        const uint32_t rank = lanes_below(tail_act);
+        uint32_t fit = 0, slot0 = 0;
+        if (tail_mode == 2) {
+            uint32_t s = 0;
+            if (lane == 0) s = __hip_atomic_fetch_add(pool.reserved, k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            slot0 = __builtin_amdgcn_readfirstlane(s);
+            fit = slot0 >= PLANE_POOL_CAP ? 0u : (PLANE_POOL_CAP - slot0 < k ? PLANE_POOL_CAP - slot0 : k);
+        }
         if ((tail_act >> lane) & 1u) {
-            uint32_t *rec = stage + PLANE_TAIL_REC * lanes_below(tail_act);
+            uint32_t v[PLANE_POOL_REC];
 #pragma unroll
-            for (int w = 0; w < 27; ++w) rec[w] = B.P[w / 3][w % 3];
-            rec[27] = (uint32_t)p;
-            rec[28] = (uint32_t)(p >> 32);
-            rec[29] = depth;
-            rec[30] = stk.lane_off;
-            rec[31] = bguess;
-            rec[32] = mst;
+            for (int w = 0; w < 27; ++w) v[w] = B.P[w / 3][w % 3];
+            v[27] = (uint32_t)p;
+            v[28] = (uint32_t)(p >> 32);
+            v[29] = depth;
+            v[30] = stk.lane_off;
+            v[31] = bguess;
+            v[32] = mst;
+            v[33] = v[34] = v[35] = 0u;
+            if (rank < fit) {
+                sdk_v4u *q = (sdk_v4u *)(pool.recs + (size_t)(slot0 + rank) * PLANE_POOL_REC);
+#pragma unroll
+                for (int i = 0; i < PLANE_POOL_REC / 4; ++i)
+                    q[i] = sdk_v4u{v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]};
+            } else {
+                uint32_t *rec = stage + PLANE_TAIL_REC * (rank - fit);
+#pragma unroll
+                for (int w = 0; w < PLANE_TAIL_REC; ++w) rec[w] = v[w];
+            }
+        }
+        if (fit) {
+            // the records are in this XCD's L2 before their flags are set
+            __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);
+            if (((tail_act >> lane) & 1u) && rank < fit)
+                __hip_atomic_store(pool.flags + slot0 + rank, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // flags set before the records count as published
+            if (lane == 0) __hip_atomic_fetch_add(pool.avail, (int32_t)fit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
         wave_lds_sync();
-        uint32_t wst[5];
-        plane_wide_tail(stage, __builtin_popcountll(tail_act), lane, stk.rsrc, io, ws, defer_list, best, node_order,
-                        mrv_after, wst);
+        uint32_t wst[5] = {0u, 0u, 0u, 0u, 0u};
+        if (k > fit)
+            plane_wide_tail(stage, (int)(k - fit), lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after,
+                            wst);
 #if SDK_PLANE_STAMPS
         st_tailp = wst[2];
 #endif
@@ -1112,6 +1283,17 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             solved += wst[0];
             guesses += wst[1];
             passes += wst[2];
+        }
+    }
+    if (tail_mode == 2) {
+        uint32_t wst[5] = {0u, 0u, 0u, 0u, 0u};
+        plane_pool_drain(pool, stage, lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after, wst);
+        if (lane == 0) {
+            solved += wst[0];
+            guesses += wst[1];
+            passes += wst[2];
+            fin -= wst[3];
+            deferred += wst[3];
         }
     }
 #if SDK_PLANE_STAMPS
@@ -1144,10 +1326,12 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     passes = wave_sum(passes);
     deferred = wave_sum(deferred);
     if (lane == 0 && deferred) atomicAdd(&ws[WS_DEFERRED], (unsigned long long)deferred);
-    if (lane == 0 && (fin | deferred)) {
-        atomicAdd(&ws[WS_FINISHED], (unsigned long long)fin);
+    if (lane == 0 && (fin | deferred | passes)) {
+        // (sign-extended: a wave that took deferred boards from the pool can
+        // end with a negative count of its own)
+        atomicAdd(&ws[WS_FINISHED], (unsigned long long)(long long)(int32_t)fin);
         atomicAdd(&ws[WS_SOLVED], (unsigned long long)solved);
-        atomicAdd(&ws[WS_GUESSES], (unsigned long long)guesses);
+        atomicAdd(&ws[WS_GUESSES], (unsigned long long)(long long)(int32_t)guesses);
         atomicAdd(&ws[WS_SWEEPS], (unsigned long long)passes);
     }
 }

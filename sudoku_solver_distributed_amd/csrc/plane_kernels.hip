@@ -39,7 +39,7 @@ int sdk_set_plane_search(int mrv_after)
 
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 {
-    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 1 || refill == 0 || chunk > PLANE_CHUNK_MAX) return -1;
+    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 2 || refill == 0 || chunk > PLANE_CHUNK_MAX) return -1;
     if (refill < 0 && tail < 0 && tail_mode < 0 && chunk < 0) {
         g_refill = g_tail = g_tail_mode = g_chunk = -1;
         return 0;

@@ -43,8 +43,11 @@
 
 // ------------------------------------------------------------- solve kernel
 // re-arm the per-call workspace words on the stream (graph-capturable)
-__global__ void arm_kernel(unsigned long long *ws)
+// pool: the plane kernel's tail pool (common.h), or null
+__global__ void arm_kernel(unsigned long long *ws, uint32_t *pool)
 {
+    if (pool && threadIdx.x < PLANE_POOL_XCDS * 4)
+        pool[(threadIdx.x >> 2) * PLANE_POOL_STRIDE + (threadIdx.x & 3)] = 0u;
     if (threadIdx.x == WS_QUEUE) ws[WS_QUEUE] = 0ull;
     if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
     if (threadIdx.x == WS_DEFER_COUNT) ws[WS_DEFER_COUNT] = 0ull;
@@ -567,9 +570,17 @@ int sdk_set_solve_kernel(int kernel)
     g_variant.store(kernel ? kernel : env_variant());
     return prev;
 }
+// the tail pool: after the stacks and the deferred list
+static uint32_t *plane_pool_base(void *d_workspace, int64_t max_threads)
+{
+    return (uint32_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads) +
+                        (size_t)PLANE_DEFER_CAP * sizeof(int64_t));
+}
+
 size_t sdk_workspace_bytes(void)
 {
-    return WS_STACK_BYTE + plane_stack_bytes(plane_max_threads()) + (size_t)PLANE_DEFER_CAP * sizeof(int64_t);
+    return WS_STACK_BYTE + plane_stack_bytes(plane_max_threads()) + (size_t)PLANE_DEFER_CAP * sizeof(int64_t) +
+           PLANE_POOL_BYTES;
 }
 
 int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status, int64_t n,
@@ -598,7 +609,7 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
         // A batch the static hand-out covers (one board per wave) never uses
         // the queue head's value, and an unordered one not the best word:
         // no re-arm launch then (a single board's latency: -1 launch)
-        if (ordered || n > max_waves) hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
+        if (ordered || n > max_waves) hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws, (uint32_t *)nullptr);
         const int64_t waves = n < max_waves ? n : max_waves;
         int64_t chunk = n / (waves * 16);
         if (chunk < 1) chunk = 1;
@@ -607,9 +618,9 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
         hipLaunchKernelGGL(solvep_kernel, dim3((unsigned)blocks), dim3(BLOCK_THREADS), 0, st, d_puzzles, d_solutions,
                            d_status, n, ws, chunk, ordered, order);
     } else {
-        hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
         // lanes: one per board up to a full grid; the stacks sit in the workspace
         const int64_t max_threads = plane_max_threads();
+        hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws, plane_pool_base(d_workspace, max_threads));
         // grid_waves > 0: at most that many waves per SIMD (4 SIMDs per CU) in
         // this launch's grid, so launches in flight on other streams are
         // co-resident with it instead of queueing behind its drain
@@ -674,8 +685,8 @@ int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutio
     hipStream_t st = (hipStream_t)stream;
     unsigned long long *ws = (unsigned long long *)d_workspace;
     std::lock_guard<std::mutex> lk(g_launch_mu);
-    hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws);
     const int64_t max_threads = plane_max_threads();
+    hipLaunchKernelGGL(arm_kernel, dim3(1), dim3(64), 0, st, ws, plane_pool_base(d_workspace, max_threads));
     const int64_t grid_cap = (int64_t)cu_count() * 4 * grid_waves * 64;
     const int64_t lane_cap = grid_waves > 0 && grid_cap < max_threads ? grid_cap : max_threads;
     const int64_t threads = total < lane_cap ? total : lane_cap;

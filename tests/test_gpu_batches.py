@@ -150,11 +150,11 @@ def test_search_mode_switch_same_results(solver, order):
         assert np.array_equal(want[0][g0:g1].cpu().numpy(), w) and np.array_equal(want[1][g0:g1].cpu().numpy(), ws)
         for k in (1, 8, 48, 128):
             assert lib.sdk_set_plane_search(k) >= 0
-            for tail in (8, 40):
-                assert lib.sdk_set_plane_tuning(-1, tail, -1, -1) == 0
+            for tail, mode in ((8, 1), (16, 2), (40, 2)):  # own tail / the XCD pool
+                assert lib.sdk_set_plane_tuning(-1, tail, mode, -1) == 0
                 got = solver.solve(p, order=order)
                 torch.cuda.synchronize()
-                assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]), (k, tail)
+                assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]), (k, tail, mode)
         # across batches, and ordered mode (frontier split semantics)
         assert lib.sdk_set_plane_search(1) >= 0
         cut = [0, 7_000, 30_500, 36_000, p.shape[0]]

@@ -448,7 +448,7 @@ def test_hard_search_4m(solver):
     assert np.array_equal(sols[idx.to(p.device)].cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("tail,mode", [(40, 1), (40, 0), (0, 1)])
+@pytest.mark.parametrize("tail,mode", [(40, 1), (40, 0), (0, 1), (40, 2), (8, 2)])
 def test_plane_tail_paths(solver, tail, mode):
     """The plane kernel's drained-wave tail (sdk_set_plane_tuning): with 40
     the most boards of every wave end on the tail solver -- wave-wide
