@@ -376,6 +376,10 @@ def main():
     ap.add_argument("--grid-waves", type=int, default=-1,
                     help="waves per SIMD in each launch's grid (sdk_solve_batch_grid; -1: the default for the "
                          "launches in flight, a full grid at --inflight 1; 0: a full grid)")
+    ap.add_argument("--pool-last", type=int, default=-1,
+                    help="launches at the end of the timed sequence that run unpipelined, their drained waves "
+                         "sharing the last boards through the XCD tail pool (-1: solve_inflight's default, "
+                         "half the launches in flight)")
     ap.add_argument("--launch-events", action="store_true",
                     help="also time each launch's own span with events on its slot stream (launch_ms)")
     ap.add_argument("--mrv-after", type=int, default=-1,
@@ -461,7 +465,8 @@ def main():
     def steps(k, events=None, inflight=m):
         solver.solve_inflight([inputs[i % group] for i in range(k)], [bufs[i % nb][0] for i in range(k)],
                               [bufs[i % nb][1] for i in range(k)], inflight=inflight, launch_events=events,
-                              grid_waves=grid_waves if inflight > 1 else 0, group=group)
+                              grid_waves=grid_waves if inflight > 1 else 0, group=group,
+                              pool_last=None if args.pool_last < 0 else args.pool_last)
 
     steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -529,7 +534,11 @@ def main():
     total = (args.batch if args.scaling == "strong" else args.batch * world) * args.steps
     value = total / wall_max
     kern_s = kern_ms / 1e3  # this GPU's share of the timed region per step
-    shape = {"boards_per_step": shard, "group": group, "inflight": m, "grid_waves": grid_waves_used}
+    # pool_last: the launches at the end that share their tails through the
+    # XCD pool (solve_inflight's default: half the launches in flight; -1 all)
+    pool_last = args.pool_last if args.pool_last >= 0 else ((m + 1) // 2 if m > 1 else -1)
+    shape = {"boards_per_step": shard, "group": group, "inflight": m, "grid_waves": grid_waves_used,
+             "pool_last": pool_last}
     roof = {"bound": "valu", "achieved": None, "peak": PEAK_VALU_OPS / 1e12, "unit": "TOP/s",
             "frac": None, "traffic": None, "kernel_ms": kern_ms, "launch_ms": launch_ms, "shape": shape,
             "hbm": {"achieved_GBps": BYTES_PER_BOARD * shard / kern_s / 1e9,

@@ -70,7 +70,13 @@ int sdk_solve_batch(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_s
  * launches are resident together, so one launch's drain (its last boards,
  * most lanes idle) runs beside the next one's start.  Results never depend on
  * it; a negative value is a bad argument (-2).  Replaces the same reference
- * walks as sdk_solve_batch (gen.py:6-28, node.py:62-74). */
+ * walks as sdk_solve_batch (gen.py:6-28, node.py:62-74).
+ * grid_waves | SDK_GRID_PIPELINED: another launch is queued behind this one
+ * on the device.  Its drained waves then finish only their own last boards
+ * and exit, so the next launch's waves take their slots; without the flag
+ * (the launch's end is the caller's wait) they share their last boards
+ * across the XCD through the tail pool (tail mode 2). */
+#define SDK_GRID_PIPELINED 0x10000
 int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t *d_status,
                          int64_t n, void *d_workspace, int order, int ordered, void *stream,
                          int grid_waves);

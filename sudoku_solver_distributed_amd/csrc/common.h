@@ -89,10 +89,10 @@ struct PlaneBatches {
 // Launch the plane kernel (plane_kernels.hip) and report its occupancy.
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
                             unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
-                            int64_t threads, hipStream_t st);
+                            int64_t threads, int pipelined, hipStream_t st);
 // the same over several batches (unordered only)
 hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws, uint32_t *stack,
-                                  int64_t *defer_list, int order, int64_t threads, hipStream_t st);
+                                  int64_t *defer_list, int order, int64_t threads, int pipelined, hipStream_t st);
 int sdk_plane_blocks_per_cu();
 #define PLANE_MAX_DEPTH 32
 // plane kernel workgroup: ONE wave.  Its waves share nothing (each has its

@@ -44,12 +44,19 @@
 #define SDK_PLANE_REFILL 3
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 16  // with the pool; 8 without (tail mode 1)
+#define SDK_PLANE_TAIL 16
 #endif
 // 2: continue on the wave-wide solver through the XCD's tail pool, 1: the
 // same on the wave's own boards only, 0: restart on the wave-per-board solver
 #ifndef SDK_PLANE_TAIL_MODE
 #define SDK_PLANE_TAIL_MODE 2
+#endif
+// a pipelined launch's (SDK_GRID_PIPELINED)
+#ifndef SDK_PLANE_PIPE_TAIL
+#define SDK_PLANE_PIPE_TAIL 8
+#endif
+#ifndef SDK_PLANE_PIPE_TAIL_MODE
+#define SDK_PLANE_PIPE_TAIL_MODE 1
 #endif
 #ifndef SDK_PLANE_CHUNK
 #define SDK_PLANE_CHUNK 64

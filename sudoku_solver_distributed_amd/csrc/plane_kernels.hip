@@ -18,7 +18,13 @@
 // continues each search, 0: the wave-per-board solver restarts it),
 // $SDK_PLANE_CHUNK most boards a wave claims from the queue at once (0: one
 // claim per refill), $SDK_PLANE_MRV passes on a board before its search
-// switches to the completion count (plane::search_step; 0: never)
+// switches to the completion count (plane::search_step; 0: never).
+// Pipelined launches (SDK_GRID_PIPELINED: another launch is queued behind)
+// take $SDK_PLANE_PIPE_TAIL / $SDK_PLANE_PIPE_TAIL_MODE instead: their
+// drained waves exit after their own tails, the next launch wants the slots
+// (pool on a pipelined launch: -5 % at 100 steps in flight; off the pipeline
+// +16 % on the N = 8 rank's runs).  sdk_set_plane_tuning's
+// tail / tail mode apply to both.
 static int env_int(const char *name, int dflt)
 {
     const char *e = getenv(name);
@@ -56,17 +62,20 @@ struct PlaneKnobs {
     uint32_t mrv_after;
 };
 
-static PlaneKnobs plane_knobs()
+static PlaneKnobs plane_knobs(int pipelined)
 {
     static const int refill_env = env_int("SDK_PLANE_REFILL", SDK_PLANE_REFILL);
     static const int tail_env = env_int("SDK_PLANE_TAIL", SDK_PLANE_TAIL);
     static const int tail_mode_env = env_int("SDK_PLANE_TAIL_MODE", SDK_PLANE_TAIL_MODE);
     static const int chunk_env = env_int("SDK_PLANE_CHUNK", SDK_PLANE_CHUNK);
     static const int mrv_env = env_int("SDK_PLANE_MRV", SDK_PLANE_MRV);
+    static const int pipe_tail_env = env_int("SDK_PLANE_PIPE_TAIL", SDK_PLANE_PIPE_TAIL);
+    static const int pipe_tail_mode_env = env_int("SDK_PLANE_PIPE_TAIL_MODE", SDK_PLANE_PIPE_TAIL_MODE);
     const int refill = g_refill >= 0 ? g_refill.load() : refill_env;
-    int tail = g_tail >= 0 ? g_tail.load() : tail_env;
+    int tail = g_tail >= 0 ? g_tail.load() : pipelined ? pipe_tail_env : tail_env;
     tail = tail > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail;
-    const int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : tail_mode_env;
+    int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : pipelined ? pipe_tail_mode_env : tail_mode_env;
+    tail_mode = tail_mode < 0 ? 0 : tail_mode > 2 ? 2 : tail_mode;  // ($SDK_PLANE_*TAIL_MODE is not range-checked)
     int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
     chunk = chunk > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : chunk;  // ($SDK_PLANE_CHUNK is not range-checked)
     int mrv = g_mrv >= 0 ? g_mrv.load() : mrv_env;
@@ -76,9 +85,9 @@ static PlaneKnobs plane_knobs()
 
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
                             unsigned long long *ws, uint32_t *stack, int64_t *defer_list, int ordered, int order,
-                            int64_t threads, hipStream_t st)
+                            int64_t threads, int pipelined, hipStream_t st)
 {
-    const PlaneKnobs k = plane_knobs();
+    const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
                        stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);
@@ -86,9 +95,9 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
 }
 
 hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws, uint32_t *stack,
-                                  int64_t *defer_list, int order, int64_t threads, hipStream_t st)
+                                  int64_t *defer_list, int order, int64_t threads, int pipelined, hipStream_t st)
 {
-    const PlaneKnobs k = plane_knobs();
+    const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel_multi, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, bs, ws, stack,
                        defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);

@@ -598,6 +598,8 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
         return -2;
     }
     if (n == 0) return 0;
+    const int pipelined = (grid_waves & SDK_GRID_PIPELINED) != 0;
+    grid_waves &= ~SDK_GRID_PIPELINED;
     hipStream_t st = (hipStream_t)stream;
     unsigned long long *ws = (unsigned long long *)d_workspace;
     int variant = solve_variant();
@@ -629,7 +631,8 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
         const int64_t threads = n < lane_cap ? n : lane_cap;
         uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
         int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
-        e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, list, ordered, order, threads, st);
+        e = sdk_launch_plane(d_puzzles, d_solutions, d_status, n, ws, stack, list, ordered, order, threads, pipelined,
+                             st);
         if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
         // the boards it left (clashing givens, deep searches): wave per board,
         // one wave per CU (its waves exit at once when nothing was left, and
@@ -682,6 +685,8 @@ int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutio
         }
         return 0;
     }
+    const int pipelined = (grid_waves & SDK_GRID_PIPELINED) != 0;
+    grid_waves &= ~SDK_GRID_PIPELINED;
     hipStream_t st = (hipStream_t)stream;
     unsigned long long *ws = (unsigned long long *)d_workspace;
     std::lock_guard<std::mutex> lk(g_launch_mu);
@@ -692,7 +697,7 @@ int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutio
     const int64_t threads = total < lane_cap ? total : lane_cap;
     uint32_t *stack = (uint32_t *)((char *)d_workspace + WS_STACK_BYTE);
     int64_t *list = (int64_t *)((char *)d_workspace + WS_STACK_BYTE + plane_stack_bytes(max_threads));
-    hipError_t e = sdk_launch_plane_multi(bs, ws, stack, list, order, threads, st);
+    hipError_t e = sdk_launch_plane_multi(bs, ws, stack, list, order, threads, pipelined, st);
     if (e != hipSuccess) return set_err("sdk_solve_batches: plane launch", e);
     const int64_t max_waves = deferred_waves();
     const int64_t groups = (total + 63) / 64;

@@ -89,6 +89,15 @@ def default_inflight():
     return (6, 1) if hwq >= 8 else (3, GRID_WAVES_INFLIGHT)
 
 
+def _grid_arg(grid_waves: int, pipelined: bool) -> int:
+    """sdk_solve_batch_grid / sdk_solve_batches' grid argument: waves per
+    SIMD, | SDK_GRID_PIPELINED for a launch with another queued behind it."""
+    g = int(grid_waves)
+    if g < 0 or g >= _lib.SDK_GRID_PIPELINED:
+        raise ValueError("grid_waves must be 0..65535")
+    return g | (_lib.SDK_GRID_PIPELINED if pipelined else 0)
+
+
 class BatchSolver:
     """One per device.  Holds the device workspace of the C ABI.
 
@@ -133,13 +142,16 @@ class BatchSolver:
 
     # -------------------------------------------------------------- solve
     def solve(self, puzzles, out: Optional[torch.Tensor] = None, status: Optional[torch.Tensor] = None,
-              ordered: bool = False, order="gen", stream=None, grid_waves: int = 0
+              ordered: bool = False, order="gen", stream=None, grid_waves: int = 0, pipelined: bool = False
               ) -> Tuple[torch.Tensor, torch.Tensor]:
         """Solve every board with the reference walk `order` ("gen":
         gen.py:6-28, "node": node.py:62-74).  Asynchronous on the stream;
         returns (solutions uint8 (n,81), status int32 (n,)).  grid_waves > 0
         caps the lane-per-board kernel's grid at that many waves per SIMD
-        (sdk_solve_batch_grid; solve_inflight's co-resident launches)."""
+        (sdk_solve_batch_grid; solve_inflight's co-resident launches).
+        pipelined: another launch follows on the device (SDK_GRID_PIPELINED:
+        drained waves exit instead of sharing the last boards); results never
+        depend on it."""
         p = self._dev(as_boards(puzzles))
         n = p.shape[0]
         if out is None:
@@ -153,11 +165,13 @@ class BatchSolver:
         with self._lock, torch.cuda.device(self.device):
             rc = self.lib.sdk_solve_batch_grid(p.data_ptr(), out.data_ptr(), status.data_ptr(), n,
                                                self.workspace.data_ptr(), _lib.order_code(order),
-                                               1 if ordered else 0, self._ws_stream(stream), int(grid_waves))
+                                               1 if ordered else 0, self._ws_stream(stream),
+                                               _grid_arg(grid_waves, pipelined))
         _lib.check(rc, "sdk_solve_batch_grid")
         return out, status
 
-    def solve_batches(self, batches, outs, statuses, order="gen", stream=None, grid_waves: int = 0):
+    def solve_batches(self, batches, outs, statuses, order="gen", stream=None, grid_waves: int = 0,
+                      pipelined: bool = False):
         """Several device batches solved by ONE launch sequence
         (sdk_solve_batches): the lane-per-board kernel's queue runs over the
         batches laid end to end and drains once, so batches too small to fill
@@ -180,7 +194,7 @@ class BatchSolver:
         ns = (ctypes.c_int64 * k)(*[p.shape[0] for p in ps])
         with self._lock, torch.cuda.device(self.device):
             rc = self.lib.sdk_solve_batches(ins, out_p, st_p, ns, k, self.workspace.data_ptr(), _lib.order_code(order),
-                                            self._ws_stream(stream), int(grid_waves))
+                                            self._ws_stream(stream), _grid_arg(grid_waves, pipelined))
         _lib.check(rc, "sdk_solve_batches")
         return list(zip(outs, statuses))
 
@@ -208,7 +222,8 @@ class BatchSolver:
             return self._slots[:inflight]
 
     def solve_inflight(self, batches, outs, statuses, inflight: Optional[int] = None, order="gen",
-                       ordered: bool = False, launch_events=None, grid_waves: Optional[int] = None, group: int = 1):
+                       ordered: bool = False, launch_events=None, grid_waves: Optional[int] = None, group: int = 1,
+                       pool_last: Optional[int] = None):
         """Solve a sequence of device batches with up to `inflight` launches
         in flight on this GPU: batch i runs on slot i % inflight (its own
         workspace and stream), so a launch's end -- its last boards draining
@@ -224,7 +239,14 @@ class BatchSolver:
         group > 1: each launch solves `group` consecutive batches at once
         (solve_batches, one queue over them; unordered only) -- the
         strong-scaling steps, where one GPU's share of a step is too small to
-        fill the GPU alone."""
+        fill the GPU alone.  The last `pool_last` launches run unpipelined
+        -- little is queued behind them, so their drained waves share the last
+        boards through the XCD tail pool; every earlier launch is pipelined
+        (its drained waves leave their slots to the launches on the other
+        streams).  Default: half the launches in flight, rounded up (three of
+        six: +1.3 % over six and over none at 20 steps, equal at 100; the
+        N = 8 rank's 20 steps +12 %); with one launch in flight
+        nothing can use the slots, so every launch shares its tail."""
         if inflight is None:
             inflight, gw = default_inflight()
             grid_waves = gw if grid_waves is None else grid_waves
@@ -246,17 +268,23 @@ class BatchSolver:
         ready.record(caller)
         for _, s in slots:
             s.wait_event(ready)
+        nl = (len(batches) + group - 1) // group
+        if pool_last is None:
+            last = nl if inflight == 1 else (inflight + 1) // 2
+        else:
+            last = max(0, pool_last)
         for i, lo in enumerate(range(0, len(batches), group)):
             solver, s = slots[i % inflight]
+            pipe = i < nl - last
             bs, os_, sts = batches[lo:lo + group], outs[lo:lo + group], statuses[lo:lo + group]
             if launch_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record(s)
             if group == 1:
                 solver.solve(bs[0], out=os_[0], status=sts[0], order=order, ordered=ordered, stream=s,
-                             grid_waves=grid_waves)
+                             grid_waves=grid_waves, pipelined=pipe)
             else:
-                solver.solve_batches(bs, os_, sts, order=order, stream=s, grid_waves=grid_waves)
+                solver.solve_batches(bs, os_, sts, order=order, stream=s, grid_waves=grid_waves, pipelined=pipe)
             if launch_events is not None:
                 e1.record(s)
                 launch_events.append((e0, e1))

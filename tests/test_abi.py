@@ -113,6 +113,7 @@ def test_solve_batch_grid_arguments():
     assert f(16, 16, 16, 1, 16, 0, 0, None, -1) == -2
     assert f(None, None, None, 0, None, 0, 0, None, 2) == 0
     assert f(None, None, None, 0, None, 7, 0, None, 2) == -2  # unknown order
+    assert f(None, None, None, 0, None, 0, 0, None, 2 | _lib.SDK_GRID_PIPELINED) == 0  # the pipelined flag
 
 
 def test_plane_tuning_rejects_oversized_chunks():

@@ -25,7 +25,8 @@ def test_default_kernel_has_matching_pmc_profile():
         inflight, grid_waves = default_inflight()
     assert pmc["kernel"] == kname
     assert pmc["seed"] == 2024 and pmc.get("workload", "hard17") == "hard17"
-    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": inflight, "grid_waves": grid_waves}
+    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": inflight, "grid_waves": grid_waves,
+                            "pool_last": (inflight + 1) // 2}
     assert pmc["counters_per_launch"]["SQ_WAVES"] == 256 * 4 * grid_waves
     assert pmc["valu_insts_per_launch"] > 0
     assert pmc["hbm_bytes_per_launch"] is None or pmc["hbm_bytes_per_launch"] > 0

@@ -175,3 +175,32 @@ def test_search_mode_switch_same_results(solver, order):
     finally:
         lib.sdk_set_plane_search(-1)
         lib.sdk_set_plane_tuning(-1, -1, -1, -1)
+
+
+def test_pipelined_flag_same_results(solver):
+    """SDK_GRID_PIPELINED (a launch with another queued behind it: drained
+    waves keep to their own tails) against the default launch (the XCD tail
+    pool): the same bytes and statuses, single- and multi-batch, and through
+    solve_inflight with every launch pipelined / none."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    p = torch.cat([hard17_batch(40_000, seed=61), hard_search_batch(20_000, seed=62)]).cuda()
+    a = [t.clone() for t in solver.solve(p)]
+    b = solver.solve(p, pipelined=True)
+    torch.cuda.synchronize()
+    assert torch.equal(a[0], b[0]) and torch.equal(a[1], b[1]) and bool((a[1] == 1).all())
+    parts = [p[:25_000], p[25_000:]]
+    for pipe in (False, True):
+        outs = [torch.empty_like(x) for x in parts]
+        sts = [torch.empty(x.shape[0], dtype=torch.int32, device=x.device) for x in parts]
+        solver.solve_batches(parts, outs, sts, grid_waves=1, pipelined=pipe)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs), a[0]) and torch.equal(torch.cat(sts), a[1])
+    steps = [p[i * 10_000:(i + 1) * 10_000] for i in range(6)]
+    for last in (0, 2, 6):
+        outs = [torch.empty_like(x) for x in steps]
+        sts = [torch.empty(x.shape[0], dtype=torch.int32, device=x.device) for x in steps]
+        solver.solve_inflight(steps, outs, sts, inflight=3, pool_last=last)
+        torch.cuda.synchronize()
+        assert torch.equal(torch.cat(outs), a[0]) and torch.equal(torch.cat(sts), a[1]), last
+    with pytest.raises(ValueError):
+        solver.solve(p[:10], grid_waves=1 << 16)
