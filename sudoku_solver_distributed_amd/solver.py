@@ -93,9 +93,9 @@ def _grid_arg(grid_waves: int, pipelined: bool) -> int:
     """sdk_solve_batch_grid / sdk_solve_batches' grid argument: waves per
     SIMD, | SDK_GRID_PIPELINED for a launch with another queued behind it."""
     g = int(grid_waves)
-    if g < 0 or g >= _lib.SDK_GRID_PIPELINED:
-        raise ValueError("grid_waves must be 0..65535")
-    return g | (_lib.SDK_GRID_PIPELINED if pipelined else 0)
+    if g >= _lib.SDK_GRID_PIPELINED:
+        raise ValueError("grid_waves must be below 65536")
+    return g | (_lib.SDK_GRID_PIPELINED if pipelined and g >= 0 else 0)  # (negative: the library's -2)
 
 
 class BatchSolver:
