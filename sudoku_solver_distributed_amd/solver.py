@@ -89,6 +89,18 @@ def default_inflight():
     return (6, 1) if hwq >= 8 else (3, GRID_WAVES_INFLIGHT)
 
 
+def pipelined_launches(n_launches: int, inflight: int, pool_last: Optional[int] = None):
+    """solve_inflight's per-launch SDK_GRID_PIPELINED flags: every launch
+    but the last `pool_last` (default: half the launches in flight, rounded
+    up; with one in flight none -- nothing can take a drained launch's
+    slots, so each shares its tail through the XCD pool)."""
+    if pool_last is None:
+        last = n_launches if inflight == 1 else (inflight + 1) // 2
+    else:
+        last = max(0, pool_last)
+    return [i < n_launches - last for i in range(n_launches)]
+
+
 def _grid_arg(grid_waves: int, pipelined: bool) -> int:
     """sdk_solve_batch_grid / sdk_solve_batches' grid argument: waves per
     SIMD, | SDK_GRID_PIPELINED for a launch with another queued behind it."""
@@ -268,14 +280,10 @@ class BatchSolver:
         ready.record(caller)
         for _, s in slots:
             s.wait_event(ready)
-        nl = (len(batches) + group - 1) // group
-        if pool_last is None:
-            last = nl if inflight == 1 else (inflight + 1) // 2
-        else:
-            last = max(0, pool_last)
+        pipes = pipelined_launches((len(batches) + group - 1) // group, inflight, pool_last)
         for i, lo in enumerate(range(0, len(batches), group)):
             solver, s = slots[i % inflight]
-            pipe = i < nl - last
+            pipe = pipes[i]
             bs, os_, sts = batches[lo:lo + group], outs[lo:lo + group], statuses[lo:lo + group]
             if launch_events is not None:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

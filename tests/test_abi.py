@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -144,3 +146,22 @@ def test_plane_search_knob_range():
         assert L.sdk_set_plane_search(-1) == 0
     finally:
         L.sdk_set_plane_search(-1)
+
+
+def test_pipelined_launch_choice():
+    """solve_inflight's SDK_GRID_PIPELINED choice (host logic): all but the
+    last half of the launches in flight; none back to back; pool_last
+    overrides; the flag is OR-ed into the grid argument, negatives pass to
+    the library's own check."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.solver import _grid_arg, pipelined_launches
+    assert pipelined_launches(10, 6) == [True] * 7 + [False] * 3
+    assert pipelined_launches(2, 6) == [False, False]
+    assert pipelined_launches(5, 1) == [False] * 5
+    assert pipelined_launches(4, 3, pool_last=0) == [True] * 4
+    assert pipelined_launches(4, 3, pool_last=1) == [True, True, True, False]
+    assert pipelined_launches(0, 6) == []
+    assert _grid_arg(1, True) == 1 | _lib.SDK_GRID_PIPELINED and _grid_arg(2, False) == 2
+    assert _grid_arg(-1, True) == -1
+    with pytest.raises(ValueError):
+        _grid_arg(1 << 16, False)
