@@ -20,13 +20,14 @@ n = int(sys.argv[1]) if len(sys.argv) > 1 else 1 << 20
 solver = get_solver("cuda:0")
 lib = solver.lib
 make = hard_search_batch if (len(sys.argv) > 2 and sys.argv[2] == "hard_search") else hard17_batch
+gw = int(sys.argv[3]) if len(sys.argv) > 3 else 0  # waves per SIMD in the grid (0: full)
 boards = make(n, seed=2024, device="cuda:0")
 for _ in range(3):
-    solver.solve(boards)
+    solver.solve(boards, grid_waves=gw)
 torch.cuda.synchronize()
 ws = solver.workspace
 ws[24 * 8:30 * 8].zero_()
-solver.solve(boards)
+solver.solve(boards, grid_waves=gw)
 torch.cuda.synchronize()
 pd = ws[24 * 8:30 * 8].view(torch.int64).cpu().numpy()
 if pd[0] or pd[1]:
@@ -35,8 +36,8 @@ cap = 1 << 20
 total = int(lib.sdk_workspace_bytes())
 pool_bytes = 8 * (32 + 8192 * 37) * 4  # PLANE_POOL_BYTES (common.h), after the deferred list
 list_off = total - pool_bytes - cap * 8
-waves = (min(n, 256 * 4 * 256)) // 64
-st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 128].view(torch.int64).cpu().numpy().reshape(-1, 16)
+waves = (min(n, 256 * 4 * 64 * (gw or 4))) // 64
+st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 256].view(torch.int64).cpu().numpy().reshape(-1, 32)
 t0 = st[:, 0].min()
 us = lambda x: (x - t0) / 100.0  # 100 MHz
 q = [0, 10, 50, 90, 99, 100]
@@ -70,3 +71,7 @@ print(f"claims per wave mean {claims.mean():.1f}; last claim size: latest 10% {l
 ld = us(st[:, 1]) >= np.percentile(us(st[:, 1]), 90)
 print(f"latest-drained 10% of waves: last claim size {last[ld].mean():.1f}, claims {claims[ld].mean():.1f}")
 print(f"  stamped kcycles per wave {cyc.mean() / 1e3:.1f} (shader clock; lifetime {life.mean():.1f} us)")
+piters, lanes = st[:, 16].sum(), st[:, 17].sum()
+print(f"pass iterations {piters / len(st):.0f} per wave, active lanes per pass iteration {lanes / max(piters, 1):.1f} of 64; "
+      f"search step {st[:, 18].sum() / max(st[:, 4].sum(), 1):.3f} of the pass+step cycles; iterations with a guess "
+      f"{st[:, 19].sum() / max(piters, 1):.2f}, with a backtrack {st[:, 20].sum() / max(piters, 1):.2f}")

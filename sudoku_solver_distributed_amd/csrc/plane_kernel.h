@@ -814,6 +814,9 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t st_t1 = 0;
     uint32_t st_after = 0, st_iters = 0;
+    // one lane's (lane 16's) passes and the active lanes summed over them,
+    // search-step cycles, iterations where some lane guessed / backtracked
+    uint64_t st_piters = 0, st_lanes = 0, st_step = 0, st_push = 0, st_pop = 0;
     // shader-clock cycles spent in the pass step / the store + refill block /
     // the tail restarts (s_memtime at wave-uniform points)
     uint64_t st_pass = 0, st_io = 0, st_tail = 0, st_tb = 0;
@@ -1186,6 +1189,10 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 
         // ---- one pass of this lane's board
         passes++;
+#if SDK_PLANE_STAMPS
+        st_lanes += (uint32_t)__builtin_popcountll(__builtin_amdgcn_ballot_w64(true));
+        st_piters++;
+#endif
         uint32_t und[3];
         const int r = plane::pass(B, und);
         if (r == plane::STUCK && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
@@ -1195,7 +1202,16 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         // guess / backtrack / search-mode switch (plane::search_step: the
         // lane solver's own step, checked on the host against the oracle)
         const uint32_t gb = bguess;
+#if SDK_PLANE_STAMPS
+        const uint32_t st_d0 = depth;
+        const uint64_t st_s0 = __builtin_amdgcn_s_memtime();
+#endif
         const int s = plane::search_step(B, und, r, depth, mst, stk, node_order, PLANE_MAX_DEPTH, mrv_after, bguess);
+#if SDK_PLANE_STAMPS
+        st_step += __builtin_amdgcn_s_memtime() - st_s0;
+        st_push += wany(bguess != gb) ? 1u : 0u;
+        st_pop += wany(depth < st_d0) ? 1u : 0u;
+#endif
         guesses += bguess - gb;
         if (s == plane::S_SOLVED) {
             state = PL_SOLVED;
@@ -1306,7 +1322,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 #if SDK_PLANE_STAMPS
     {
         st_tail = __builtin_amdgcn_s_memtime() - st_tt;
-        int64_t *st = defer_list + (PLANE_DEFER_CAP / 2) + 16 * (g >> 6);
+        int64_t *st = defer_list + (PLANE_DEFER_CAP / 2) + 32 * (g >> 6);
         const uint64_t t2 = __builtin_amdgcn_s_memrealtime();
         if (lane == 0) st[0] = (int64_t)st_t0;
         if (lane == 1) st[1] = (int64_t)(st_t1 ? st_t1 : t2);
@@ -1324,6 +1340,11 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         if (lane == 13) st[13] = (int64_t)st_tailn;
         if (lane == 14) st[14] = (int64_t)st_tailp;
         if (lane == 15) st[15] = (int64_t)st_claims;
+        if (lane == 16) st[16] = (int64_t)st_piters;
+        if (lane == 17) st[17] = (int64_t)st_lanes;
+        if (lane == 18) st[18] = (int64_t)st_step;
+        if (lane == 19) st[19] = (int64_t)st_push;
+        if (lane == 20) st[20] = (int64_t)st_pop;
     }
 #endif
     // per-wave statistics: the lanes' counts summed, one atomic per counter and wave
