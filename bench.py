@@ -234,7 +234,11 @@ def e2e_rate(solver, boards, reps: int = 3):
     return res
 
 
-def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
+# waves per SIMD of the grouped (multi-step) launches of sharded steps
+GRID_WAVES_GROUPED = 2
+
+
+def shard_rates(solver, boards, launch_boards: int = 1 << 21, reps: int = 3):
     """configs[2]'s per-GPU regime under strong scaling, on one GPU: steps of
     B/2, B/4, B/8 boards (a rank's shard of the B-board step at N = 2, 4, 8),
     either one step per launch (`ungrouped`) or
@@ -259,7 +263,8 @@ def shard_rates(solver, boards, launch_boards: int = 1 << 20, reps: int = 3):
 
             def run(kk):
                 solver.solve_inflight([parts[i % div] for i in range(kk)], [bufs[i % nb][0] for i in range(kk)],
-                                      [bufs[i % nb][1] for i in range(kk)], inflight=m, group=g)
+                                      [bufs[i % nb][1] for i in range(kk)], inflight=m, group=g,
+                                      grid_waves=GRID_WAVES_GROUPED if g > 1 else None)
             run(2 * g)
             best = None
             for _ in range(reps):
@@ -358,9 +363,10 @@ def main():
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
                     help="strong: --batch boards per step sharded over the ranks (BASELINE configs[2]); "
                          "weak: --batch boards per GPU per step")
-    ap.add_argument("--launch-boards", type=int, default=1 << 20,
+    ap.add_argument("--launch-boards", type=int, default=-1,
                     help="a launch solves consecutive steps' shards together (sdk_solve_batches, <= 16 steps) "
-                         "until it holds this many boards; 0 = one step per launch")
+                         "until it holds this many boards; 0 = one step per launch; -1: 2^21 when a rank's "
+                         "shard is below 2^20 boards (strong scaling, N > 1), else one step per launch")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--workload", choices=("hard17", "hard_search"), default="hard17",
                     help="timed boards: BASELINE's hard 17-clue set (default, the metric's config) or the "
@@ -432,8 +438,12 @@ def main():
     shard = hi - lo  # this rank's boards per step
     if shard <= 0:
         raise SystemExit("--batch too small for the number of ranks")
-    # steps per launch: enough consecutive steps' shards to fill a launch
-    group = 1 if args.launch_boards <= shard else min(16, -(-args.launch_boards // shard))
+    # steps per launch: enough consecutive steps' shards to fill a launch.
+    # Sharded steps (N > 1) go 2^21 boards to a launch at 2 waves per SIMD:
+    # fewer launches, so fewer drains at the end of the run (one rank of
+    # N = 2 / 4 / 8 at 20 steps: +6 / +6 / +5 % over 2^20 at 1 wave)
+    launch_boards = args.launch_boards if args.launch_boards >= 0 else (1 << 21 if shard < (1 << 20) else 0)
+    group = 1 if launch_boards <= shard else min(16, -(-launch_boards // shard))
     # one input per step of a launch group (each step its own boards): step
     # batch j is synthetic batch seed + 7919 j; strong: this rank's [lo, hi)
     # of it (the same global batch on every rank), weak: per-rank seeds
@@ -458,6 +468,8 @@ def main():
         grid_waves = args.grid_waves
     elif m == 1:
         grid_waves = 0
+    elif group > 1 and args.inflight < 0:
+        grid_waves = GRID_WAVES_GROUPED
     else:
         grid_waves = gw_def if args.inflight < 0 else (1 if m >= 5 else 2)
     grid_waves_used = grid_waves

@@ -74,9 +74,11 @@ def test_bench_two_rank_path_runs():
     assert len(lines) == 1 and not [l for l in outs[1].splitlines() if l.startswith("{")]
     d = json.loads(lines[0])
     # strong scaling (the default): the 2^20-board step split over the two
-    # ranks, each rank's launches holding two steps' shards
+    # ranks, each rank's launches holding 2^21 boards (four steps' shards) at
+    # 2 waves per SIMD
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["dist_backend"] == "gloo"
     assert d["config"]["global_batch"] == 1 << 20 and d["config"]["boards_per_gpu_per_step"] == 1 << 19
-    assert d["config"]["steps_per_launch"] == 2 and d["roofline"]["kernel"] == "plane_kernel_multi"
+    assert d["config"]["steps_per_launch"] == 4 and d["roofline"]["kernel"] == "plane_kernel_multi"
+    assert d["config"]["grid_waves_per_simd"] == 2
     assert d["side_configs"]["pathological"]["ranks"] == 2 and d["side_configs"]["pathological"]["identical"]
     assert d["all_solved_and_checked"] and d["value"] > 0
