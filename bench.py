@@ -561,7 +561,9 @@ def main():
     if group > 1 and kname == "plane_kernel":
         kname = "plane_kernel_multi"  # sdk_solve_batches' kernel
     roof["kernel"] = kname
-    PMC_FILE = os.path.join(PMC_DIR, f"pmc_{kname}.json")
+    # the metric's workload, or another one's own profile (scripts/gpu_pmc.sh names them so)
+    PMC_FILE = os.path.join(PMC_DIR, f"pmc_{kname}.json" if args.workload == "hard17"
+                            else f"pmc_{kname}_{args.workload}.json")
     roof["pmc_match"] = False
     if os.path.exists(PMC_FILE):
         with open(PMC_FILE) as f:
