@@ -7,8 +7,8 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 120 --timeout-method threa
   "tests/test_gpu_parity.py::test_hard17_vs_unique_oracle" "tests/test_gpu_parity.py::test_hard_search_vs_unique_oracle" > gpurun_out/refill_tests.log 2>&1 || { tail -30 gpurun_out/refill_tests.log; exit 1; }
 tail -2 gpurun_out/refill_tests.log
 B="--steps 20 --warmup 3 --no-cpu --no-extras --latency-boards 0 --no-serial"
-for r in 1 2; do
-for t in default refill0 oldpool lanes64; do
+for r in 1 2 3; do
+for t in default fifo; do
   if [ "$t" = default ]; then L=$PWD/sudoku_solver_distributed_amd/libsudoku_hip.so; else L=$PWD/sudoku_solver_distributed_amd/libsudoku_hip_$t.so; fi
   for mode in "n1;" "b2b;--inflight 1" "r8;--scaling weak --batch 131072"; do
     tag=${mode%%;*}; flags=${mode#*;}
