@@ -504,6 +504,35 @@ def test_solve_host_pipelined(solver):
     assert torch.equal(got, want[:5].cpu())
 
 
+def test_pool_overflow_keeps_boards_local(solver):
+    """The XCD tail pool full: a full grid (512 waves per XCD) handing over
+    up to 40 boards each reserves more than the pool's 8192 slots per XCD,
+    and the boards past them stay in their wave's LDS for its own wide
+    solver.  2^19 hard 17-clue boards against their unique completion, the
+    kernel's finished count, and the same batch with the pool off."""
+    from sudoku_solver_distributed_amd import _lib
+    from sudoku_solver_distributed_amd.gen import hard17_batch
+    lib = solver.lib
+    prev = lib.sdk_set_solve_kernel(_lib.SDK_KERNELS["plane"])
+    p = hard17_batch(1 << 19, seed=91)
+    want, cnt = O.solve_unique_batch(p.numpy())
+    assert (cnt == 1).all()
+    try:
+        assert lib.sdk_set_plane_tuning(-1, 40, 2, -1) == 0
+        solver.stats(reset=True)
+        sols, st = solver.solve(p)
+        torch.cuda.synchronize()
+        assert (st.cpu().numpy() == 1).all() and np.array_equal(sols.cpu().numpy(), want)
+        assert solver.stats()["finished"] == p.shape[0]
+        assert lib.sdk_set_plane_tuning(-1, 40, 1, -1) == 0
+        s1, t1 = solver.solve(p)
+        torch.cuda.synchronize()
+        assert torch.equal(s1, sols) and torch.equal(t1, st)
+    finally:
+        lib.sdk_set_plane_tuning(-1, -1, -1, -1)
+        lib.sdk_set_solve_kernel(prev)
+
+
 @pytest.mark.parametrize("refill,chunk", [(1, 0), (64, 64)])
 def test_plane_refill_extremes(solver, refill, chunk):
     """The plane kernel's I/O at extreme knobs (sdk_set_plane_tuning):
