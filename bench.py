@@ -445,14 +445,15 @@ def main():
     launch_boards = args.launch_boards if args.launch_boards >= 0 else (1 << 21 if shard < (1 << 20) else 0)
     group = 1 if launch_boards <= shard else min(16, -(-launch_boards // shard))
     # one input per step of a launch group (each step its own boards): step
-    # batch j is synthetic batch seed + 7919 j; strong: this rank's [lo, hi)
-    # of it (the same global batch on every rank), weak: per-rank seeds
+    # j's batch is the synthetic batch rotated by 7919 j boards (one
+    # generation however many steps a launch holds); strong: this rank's
+    # [lo, hi) of it (the same global batch on every rank), weak: per-rank seeds
+    full = make(args.batch, seed=args.seed + (rank if args.scaling == "weak" else 0))
     inputs = []
     for j in range(group):
-        sd = args.seed + 7919 * j + (rank if args.scaling == "weak" else 0)
-        full = make(args.batch, seed=sd)
-        inputs.append(full[lo:hi].contiguous().to(dev))
-        del full
+        idx = (torch.arange(lo, hi) + 7919 * j) % args.batch
+        inputs.append(full[idx].contiguous().to(dev))
+    del full
     boards = inputs[0]
     from sudoku_solver_distributed_amd.solver import default_inflight
     m_def, gw_def = default_inflight()
