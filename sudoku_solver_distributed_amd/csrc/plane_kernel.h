@@ -44,7 +44,7 @@
 #define SDK_PLANE_REFILL 3
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 16
+#define SDK_PLANE_TAIL 12
 #endif
 // 2: continue on the wave-wide solver through the XCD's tail pool, 1: the
 // same on the wave's own boards only, 0: restart on the wave-per-board solver
