@@ -403,6 +403,12 @@ def main():
     ap.add_argument("--device-index", type=int, default=None,
                     help="put every rank on cuda:<index> instead of cuda:<LOCAL_RANK> (rehearsal of the "
                          "multi-rank path on a one-GPU box)")
+    ap.add_argument("--emulate-world", type=int, default=0,
+                    help="one process on one GPU runs rank --emulate-rank of a strong-scaling job of this many "
+                         "ranks: that rank's own shard_bounds shard, step rotation and launch shape, no "
+                         "collectives; the line reports that rank's wall time (scripts/rank_emul.py runs every "
+                         "rank and takes the max).  Diagnostic: not the metric")
+    ap.add_argument("--emulate-rank", type=int, default=0)
     args = ap.parse_args()
 
     import torch
@@ -413,6 +419,11 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    emulated = args.emulate_world > 0
+    if emulated and (world != 1 or args.scaling != "strong" or not 0 <= args.emulate_rank < args.emulate_world):
+        raise SystemExit("--emulate-world: one process, --scaling strong, 0 <= --emulate-rank < --emulate-world")
+    # the job whose shard this process runs: the real one, or the emulated rank's
+    job_world, job_rank = (args.emulate_world, args.emulate_rank) if emulated else (world, rank)
     gpu = local if args.device_index is None else args.device_index
     torch.cuda.set_device(gpu)
     dev = torch.device("cuda", gpu)
@@ -432,7 +443,7 @@ def main():
         solver.lib.sdk_set_plane_search(args.mrv_after)
     make = hard17_batch if args.workload == "hard17" else hard_search_batch
     if args.scaling == "strong":
-        lo, hi = shard_bounds(args.batch, rank, world)
+        lo, hi = shard_bounds(args.batch, job_rank, job_world)
     else:
         lo, hi = 0, args.batch
     shard = hi - lo  # this rank's boards per step
@@ -506,6 +517,13 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps
     launch_ms = sum(a.elapsed_time(b) for a, b in launches) / len(launches) if launches else None
     st = solver.inflight_stats()
+    # every board of every timed step answered exactly once: the kernels'
+    # own accounting (sdk_verify_workspace raises on a board a kernel took
+    # and could not finish, e.g. a tail-pool record never published) and
+    # the finished count against the boards the steps handed out
+    solver.verify_inflight()
+    if st["finished"] != args.steps * shard:
+        raise SystemExit(f"timed steps: {st['finished']} boards answered, {args.steps * shard} handed out")
     t = torch.tensor([wall], dtype=torch.float64, device=comm_dev)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -523,6 +541,7 @@ def main():
         steps(args.steps, inflight=1)
         torch.cuda.synchronize(dev)
         s_wall = time.perf_counter() - s0
+        solver.verify_inflight()
         serial = {"value": shard * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3}
 
     # single-board latency (p50 over 32 boards, one launch each)
@@ -537,7 +556,8 @@ def main():
     lat.sort()
     p50 = lat[len(lat) // 2] if lat else None
 
-    extras = None if args.no_extras else side_configs(solver, dev, world, rank, boards, serving=not args.no_serving)
+    extras = (None if args.no_extras or emulated
+              else side_configs(solver, dev, world, rank, boards, serving=not args.no_serving))
 
     if rank != 0:
         if world > 1:
@@ -545,13 +565,17 @@ def main():
         return
 
     total = (args.batch if args.scaling == "strong" else args.batch * world) * args.steps
+    if emulated:
+        total = shard * args.steps  # this rank's boards (the job's value is the max over ranks)
     value = total / wall_max
     kern_s = kern_ms / 1e3  # this GPU's share of the timed region per step
     # pool_last: the launches at the end that share their tails through the
     # XCD pool (solve_inflight's default: half the launches in flight; -1 all)
     pool_last = args.pool_last if args.pool_last >= 0 else ((m + 1) // 2 if m > 1 else -1)
+    # (hw_queues: the process's hardware queues, which decide whether the
+    # launches in flight run side by side -- bench.py sets 8, HIP's default is 4)
     shape = {"boards_per_step": shard, "group": group, "inflight": m, "grid_waves": grid_waves_used,
-             "pool_last": pool_last}
+             "pool_last": pool_last, "hw_queues": int(os.environ["GPU_MAX_HW_QUEUES"])}
     roof = {"bound": "valu", "achieved": None, "peak": PEAK_VALU_OPS / 1e12, "unit": "TOP/s",
             "frac": None, "traffic": None, "kernel_ms": kern_ms, "launch_ms": launch_ms, "shape": shape,
             "hbm": {"achieved_GBps": BYTES_PER_BOARD * shard / kern_s / 1e9,
@@ -562,51 +586,58 @@ def main():
     if group > 1 and kname == "plane_kernel":
         kname = "plane_kernel_multi"  # sdk_solve_batches' kernel
     roof["kernel"] = kname
-    # the metric's workload, or another one's own profile (scripts/gpu_pmc.sh names them so)
-    PMC_FILE = os.path.join(PMC_DIR, f"pmc_{kname}.json" if args.workload == "hard17"
-                            else f"pmc_{kname}_{args.workload}.json")
-    roof["pmc_match"] = False
-    if os.path.exists(PMC_FILE):
-        with open(PMC_FILE) as f:
-            pmc = json.load(f)
-        # the counters count only if they were taken on EXACTLY this launch
-        # shape (scripts/gpu_pmc.sh runs this bench with the same flags)
-        if (pmc.get("kernel") == kname and pmc.get("seed") == args.seed
-                and pmc.get("workload", "hard17") == args.workload and pmc.get("shape") == shape):
-            roof["pmc_match"] = True
-            valu_step = pmc["valu_insts_per_launch"] / group  # a launch is `group` steps
-            ops = valu_step * 64
-            roof["achieved"] = ops / kern_s / 1e12
-            roof["frac"] = roof["achieved"] / roof["peak"]
-            roof["valu_insts_per_step"] = valu_step
-            if pmc.get("hbm_bytes_per_launch") is not None:
-                roof["traffic"] = pmc["hbm_bytes_per_launch"] / group
-                roof["traffic_over_algorithmic"] = roof["traffic"] / (BYTES_PER_BOARD * shard)
-            for k in ("sq_wait_inst_any_share", "sq_wait_any_share"):
-                if k in pmc:
-                    roof[k] = pmc[k]
-            roof["pmc_source"] = os.path.relpath(PMC_FILE, ROOT)
-            # lanes doing pass work: passes x VALU per pass (ISA count of
-            # plane::pass) over every lane slot the kernel issued
-            isa = os.path.join(PMC_DIR, "isa_plane_pass.json")
-            if kname.startswith("plane_kernel") and os.path.exists(isa):
-                with open(isa) as f:
-                    vpp = json.load(f)["valu_per_pass"]
-                useful = st["sweeps"] / args.steps * vpp
-                roof["valu_per_pass"] = vpp
-                roof["useful_lane_frac"] = useful / ops
-                roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
-            # the pass's own ceiling at the kernel's occupancy (microbenchmark)
-            ceil = os.path.join(PMC_DIR, "r02_pass_ceiling.json")
-            if kname.startswith("plane_kernel") and os.path.exists(ceil):
-                with open(ceil) as f:
-                    c = json.load(f)
-                cp = c["by_waves_per_simd"][str(c["plane_kernel_waves_per_simd"])]["passes_per_s"]
-                roof["pass_ceiling_passes_per_s"] = cp
-                roof["pass_ceiling_frac"] = st["sweeps"] / args.steps / kern_s / cp
+    # the committed PMC summaries of this kernel (scripts/gpu_pmc.sh: one per
+    # workload and launch shape, e.g. pmc_plane_kernel_multi_w8.json for the
+    # N = 8 rank's grouped launches); the counters count only if they were
+    # taken on EXACTLY this workload and launch shape
+    import glob
+    pmc, PMC_FILE = None, None
+    for f_ in sorted(glob.glob(os.path.join(PMC_DIR, f"pmc_{kname}*.json"))):
+        with open(f_) as f:
+            cand = json.load(f)
+        if (cand.get("kernel") == kname and cand.get("seed") == args.seed
+                and cand.get("workload", "hard17") == args.workload and cand.get("shape") == shape):
+            pmc, PMC_FILE = cand, f_
+            break
+    roof["pmc_match"] = pmc is not None
+    if pmc is not None:
+        # per step: the profiled run's dispatches summed over its steps
+        # (grouped launches hold different step counts), else per launch
+        valu_step = pmc.get("valu_insts_per_step") or pmc["valu_insts_per_launch"] / group
+        ops = valu_step * 64
+        roof["achieved"] = ops / kern_s / 1e12
+        roof["frac"] = roof["achieved"] / roof["peak"]
+        roof["valu_insts_per_step"] = valu_step
+        hbm_step = pmc.get("hbm_bytes_per_step") or (pmc["hbm_bytes_per_launch"] / group
+                                                    if pmc.get("hbm_bytes_per_launch") is not None else None)
+        if hbm_step is not None:
+            roof["traffic"] = hbm_step
+            roof["traffic_over_algorithmic"] = roof["traffic"] / (BYTES_PER_BOARD * shard)
+        for k in ("sq_wait_inst_any_share", "sq_wait_any_share"):
+            if k in pmc:
+                roof[k] = pmc[k]
+        roof["pmc_source"] = os.path.relpath(PMC_FILE, ROOT)
+        # lanes doing pass work: passes x VALU per pass (ISA count of
+        # plane::pass) over every lane slot the kernel issued
+        isa = os.path.join(PMC_DIR, "isa_plane_pass.json")
+        if kname.startswith("plane_kernel") and os.path.exists(isa):
+            with open(isa) as f:
+                vpp = json.load(f)["valu_per_pass"]
+            useful = st["sweeps"] / args.steps * vpp
+            roof["valu_per_pass"] = vpp
+            roof["useful_lane_frac"] = useful / ops
+            roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
+        # the pass's own ceiling at the kernel's occupancy (microbenchmark)
+        ceil = os.path.join(PMC_DIR, "r02_pass_ceiling.json")
+        if kname.startswith("plane_kernel") and os.path.exists(ceil):
+            with open(ceil) as f:
+                c = json.load(f)
+            cp = c["by_waves_per_simd"][str(c["plane_kernel_waves_per_simd"])]["passes_per_s"]
+            roof["pass_ceiling_passes_per_s"] = cp
+            roof["pass_ceiling_frac"] = st["sweeps"] / args.steps / kern_s / cp
 
     cpu = None
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and not emulated:
         sample = boards[:8192].cpu().numpy()
         done, el, threads = cpu_baseline(sample, args.cpu_budget)
         cpu = {"value": done / el, "unit": "boards/s", "cores": threads, "kind": "port",
@@ -615,7 +646,9 @@ def main():
                          f"literal gen.py:6-28 walk each (oracle/sudoku_oracle.c)"}
 
     line = {
-        "metric": "puzzles solved/sec (node), 1M hard 9x9 batch @1/2/4/8 GPU; single-puzzle p50 ms",
+        "metric": "puzzles solved/sec (node), 1M hard 9x9 batch @1/2/4/8 GPU; single-puzzle p50 ms"
+                  + (f" [EMULATED rank {job_rank} of {job_world} on one GPU: value = that rank's boards/s]"
+                     if emulated else ""),
         "value": value,
         "unit": "boards/s",
         "n_gpus": world,
@@ -635,7 +668,9 @@ def main():
                    "global_batch": args.batch if args.scaling == "strong" else args.batch * world,
                    "boards_per_gpu_per_step": shard, "parallelism": f"shard{world}",
                    "steps_per_launch": group, "inflight_per_gpu": m, "grid_waves_per_simd": grid_waves_used or None,
-                   "dist_backend": args.dist_backend if world > 1 else None},
+                   "dist_backend": args.dist_backend if world > 1 else None,
+                   **({"emulated_rank": job_rank, "emulated_world": job_world, "rank_wall_s": wall_max}
+                      if emulated else {})},
         "serial": serial,  # this GPU's steps back to back (rank 0's boards / s)
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,

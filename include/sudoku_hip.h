@@ -163,8 +163,22 @@ int sdk_expand_frontier(const uint8_t *d_nodes, int64_t n, uint8_t *d_tmp, int64
  * index in ordered mode (INT64_MAX if none), out[5] boards the plane kernel
  * handed to the wave-per-board pass (clashing givens, searches deeper than
  * its stack, the last few boards of a wave once the queue is empty).
- * reset != 0 zeroes them afterwards. */
+ * reset != 0 zeroes them afterwards (and the boards-assigned count of
+ * sdk_verify_workspace; never its error word). */
 int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
+
+/* Every board answered?  (Synchronous on `stream`; library extension, the
+ * reference's walk answers every board it is given, gen.py:6-28.)  Each
+ * solve launch adds its board count to the workspace, each board's answer
+ * (any status) counts once as finished, and a kernel that could not finish a
+ * board it had taken sets an error word (SDK_ERR_* bits: 1 = a tail-pool
+ * record it had claimed was never published).  out (may be
+ * NULL): out[0] boards assigned, out[1] boards finished, out[2] error bits,
+ * all since the last sdk_read_stats(reset) / report.  Returns 0 when
+ * assigned == finished and no error bit is set; -3 otherwise (text in
+ * sdk_last_error(); the error word is then cleared and the counts re-synced,
+ * so each fault is reported once); -1 HIP error; -2 bad arguments. */
+int sdk_verify_workspace(void *d_workspace, int64_t out[3], void *stream);
 
 /* The same six counters as sdk_read_stats, copied to DEVICE memory d_out[6]
  * asynchronously on `stream` (stream-ordered with the solves on that
@@ -205,8 +219,9 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk);
  * means none for the walk too, two send the board back to the walk's own
  * branch order.  0 keeps every board on the walk's order; -1
  * restores the default ($SDK_PLANE_MRV, built-in 64).  Results never
- * depend on it.  Returns the previous setting (-1: default), -1 for an
- * out-of-range value (nothing changed). */
+ * depend on it.  Returns the setting in effect before the call (the
+ * default's value when no override was set), -2 for an out-of-range value
+ * (nothing changed). */
 int sdk_set_plane_search(int mrv_after);
 
 /* Library / device info. */

@@ -28,6 +28,11 @@ def load(d):
 def main():
     out, batch, seed, dirs = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), sys.argv[4:]
     kernel = os.environ.get("PMC_KERNEL", "")
+    # PMC_STEPS: the profiled bench's steps (run with --warmup 0): per-step
+    # totals over EVERY dispatch of the kernel -- grouped launches (N > 1
+    # ranks) hold different numbers of steps, so a per-launch mean would not do
+    steps = int(os.environ.get("PMC_STEPS", "0"))
+    totals = defaultdict(float)
     vals = defaultdict(list)
     grids = set()
     for d in dirs:
@@ -41,6 +46,7 @@ def main():
         grids.add(gmax)
         per = defaultdict(float)
         for r in rows:
+            totals[r["Counter_Name"]] += float(r["Counter_Value"])
             if int(r.get("Grid_Size", 0) or 0) != gmax:
                 continue
             per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
@@ -66,6 +72,12 @@ def main():
            "hbm_bytes_per_launch": None}
     if "FETCH_SIZE" in summary and "WRITE_SIZE" in summary:
         res["hbm_bytes_per_launch"] = (2 * summary["FETCH_SIZE"] + summary["WRITE_SIZE"]) * 1024
+    if steps:
+        res["steps"] = steps
+        res["counters_per_step"] = {k: v / steps for k, v in totals.items()}
+        res["valu_insts_per_step"] = totals.get("SQ_INSTS_VALU", 0.0) / steps or None
+        if "FETCH_SIZE" in totals and "WRITE_SIZE" in totals:
+            res["hbm_bytes_per_step"] = (2 * totals["FETCH_SIZE"] + totals["WRITE_SIZE"]) * 1024 / steps
     if "SQ_WAVE_CYCLES" in summary:
         for k in ("SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY"):
             if k in summary:

@@ -36,6 +36,7 @@ EXPORTS = (
     "sdk_expand_frontier",
     "sdk_read_stats",
     "sdk_snapshot_stats",
+    "sdk_verify_workspace",
     "sdk_last_error",
     "sdk_version",
     "sdk_device_cu_count",
@@ -90,6 +91,8 @@ def load() -> ctypes.CDLL:
     L.sdk_read_stats.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), i32, vp]
     L.sdk_snapshot_stats.restype = i32
     L.sdk_snapshot_stats.argtypes = [vp, vp, vp]
+    L.sdk_verify_workspace.restype = i32
+    L.sdk_verify_workspace.argtypes = [vp, ctypes.POINTER(ctypes.c_int64), vp]
     L.sdk_last_error.restype = ctypes.c_char_p
     L.sdk_last_error.argtypes = []
     L.sdk_version.restype = ctypes.c_char_p

@@ -23,14 +23,21 @@ enum {
     WS_DEFER_COUNT = 2,  // boards the plane kernel handed back (list entries, re-armed)
     WS_DEFER_OVER = 3,   // 1: the list overflowed, every deferred board is found by status (re-armed)
     WS_ARM_WORDS = 4,    // words re-armed per call
+    WS_GEN = 4,          // launch generation (low 32 bits, never 0): arm_kernel adds one per call; the
+                         // tail pool's ready flags hold it, so a flag left by an earlier launch never reads as set
+    WS_ERR_SLOT = 5,     // diagnostic: the pool slot of the last flag-wait timeout
     WS_STACK_BYTE = 256, // the plane kernel's per-lane stacks start here, then the deferred list
     WS_FINISHED = 8,   // statistics (accumulate until sdk_read_stats(reset))
     WS_SOLVED = 9,
     WS_GUESSES = 10,
     WS_SWEEPS = 11,
     WS_DEFERRED = 12,  // boards the plane kernel left to the packed kernel
+    WS_ASSIGNED = 13,  // boards handed to the solve kernels (each launch adds its n): == WS_FINISHED once done
+    WS_ERROR = 14,     // SDK_ERR_* bits, sticky until sdk_verify_workspace reports them
     WS_WORDS = 16
 };
+// WS_ERROR bits
+#define SDK_ERR_POOL_WAIT 1u  // a pool consumer gave up waiting on a claimed record: that board was not solved
 
 __device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
 
@@ -110,9 +117,10 @@ int sdk_plane_blocks_per_cu();
 // The drained waves' tail pool (plane_kernel.h, tail mode 2), after the
 // deferred list: per XCD, a 128-byte control line (reserved / published /
 // taken counts, re-armed every call), PLANE_POOL_CAP records of
-// PLANE_POOL_REC dwords, then one ready flag (uint32) per record.  A
-// consumer clears the flag it read, so the flags are zero again at the end
-// of every launch.
+// PLANE_POOL_REC dwords, then one ready flag (uint32) per record.  A ready
+// flag holds the launch generation (WS_GEN) of the record it publishes, so
+// flags need no clearing: one left by an earlier launch (or set after its
+// consumer gave up) never matches a later launch's generation.
 #define PLANE_POOL_XCDS 8
 #define PLANE_POOL_CAP 8192
 #define PLANE_POOL_REC 36

@@ -643,14 +643,18 @@ __device__ __forceinline__ PlanePool plane_pool(int64_t *defer_list)
 
 // Take records from the pool until it is empty (wave-uniform).  A taken slot
 // has a producer that reserved it and writes it without waiting on anything,
-// so the flag wait is short; it is bounded all the same (~1 s) and a wave
-// that gives up leaves the pool.
+// so the flag wait is short (a flag holds the launch generation `gen`, so a
+// flag an earlier launch left never reads as set).  It is bounded all the
+// same (`polls` polls, ~1 s by default): a wave that gives up sets
+// SDK_ERR_POOL_WAIT in the workspace -- that record's board is not solved,
+// and sdk_verify_workspace turns the word into a failed call -- and leaves
+// the pool.
 template <class IO>
 __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t *stage, int lane,
                                               __amdgpu_buffer_rsrc_t stack_rsrc, const IO &io,
                                               unsigned long long *__restrict__ ws, int64_t *__restrict__ defer_list,
                                               const int64_t *best, int node_order, uint32_t mrv_after,
-                                              uint32_t (&st)[5])
+                                              uint32_t gen, uint32_t polls, uint32_t (&st)[5])
 {
 #if SDK_PLANE_STAMPS
     // diagnostic: claims, backed-out claims, flag polls; cycles claiming, waiting, solving (ws words 24..29)
@@ -684,17 +688,25 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
             d_t = t1;
         }
 #endif
-        uint32_t f = 0;
-        for (uint32_t tries = 0; tries < (1u << 23); ++tries) {
+        bool ready = false;
+        for (uint32_t tries = 0; tries < polls; ++tries) {
+            uint32_t f = 0;
             if (lane == 0) f = __hip_atomic_load(pool.flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            f = __builtin_amdgcn_readfirstlane(f);
+            ready = __builtin_amdgcn_readfirstlane(f) == gen;
 #if SDK_PLANE_STAMPS
             d_poll++;
 #endif
-            if (f) break;
+            if (ready) break;
             __builtin_amdgcn_s_sleep(2);
         }
-        if (!f) break;
+        if (!ready) {
+            // loud, never silent: the host's sdk_verify_workspace raises on it
+            if (lane == 0) {
+                atomicOr(&ws[WS_ERROR], (unsigned long long)SDK_ERR_POOL_WAIT);
+                __hip_atomic_store(&ws[WS_ERR_SLOT], (unsigned long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+            break;
+        }
 #if SDK_PLANE_STAMPS
         {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -712,7 +724,6 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
                                                                      __HIP_MEMORY_SCOPE_AGENT)
                                                  : 0u;
         if (lane < PLANE_TAIL_REC) stage[lane] = w;
-        if (lane == 0) __hip_atomic_store(pool.flags + h, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         wave_lds_sync();
         uint32_t wst[5];
         plane_wide_tail(stage, 1, lane, stack_rsrc, io, ws, defer_list, best, node_order, mrv_after, wst);
@@ -765,9 +776,13 @@ template <class IO>
 __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__restrict__ ws,
                                            uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list,
                                            int ordered, int order, int refill, int tail, int tail_mode, int chunk,
-                                           uint32_t mrv_after)
+                                           uint32_t mrv_after, uint32_t pool_polls)
 {
+    // (the per-byte deposit path stages one batch segment per claim; only
+    // the converted-records path splits claims at batch boundaries)
+    static_assert(SDK_PLANE_PRECONV || !IO::multi, "SDK_PLANE_PRECONV=0 supports one batch per launch only");
     const int64_t n = io.total();  // boards of the launch (virtual indices 0..n-1)
+    if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ws[WS_ASSIGNED], (unsigned long long)n);  // sdk_verify_workspace
     __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     __shared__ __attribute__((aligned(16))) uint32_t outbox_lds[PLANE_THREADS / 64][PLANE_OUTBOX * PLANE_OB_WORDS];
@@ -1237,6 +1252,8 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     // tail mode 2: the tail boards go to this XCD's pool, which every wave
     // of the XCD drains before it exits (plane_pool_drain)
     const PlanePool pool = plane_pool(defer_list);
+    // this launch's generation (arm_kernel, an earlier launch on the stream)
+    const uint32_t gen = tail_mode == 2 ? __builtin_amdgcn_readfirstlane((uint32_t)ws[WS_GEN]) : 0u;
     if (tail_act && tail_mode) {
         // ---- wave-wide tail: the lanes' boards go to LDS records (27 plane
         // words, index, depth, stack line, guesses; stride 33 dwords, so the
@@ -1278,7 +1295,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             // the records are in this XCD's L2 before their flags are set
             __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);
             if (((tail_act >> lane) & 1u) && rank < fit)
-                __hip_atomic_store(pool.flags + slot0 + rank, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                __hip_atomic_store(pool.flags + slot0 + rank, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // flags set before the records count as published
             if (lane == 0) __hip_atomic_fetch_add(pool.avail, (int32_t)fit, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
@@ -1310,7 +1327,8 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     }
     if (tail_mode == 2) {
         uint32_t wst[5] = {0u, 0u, 0u, 0u, 0u};
-        plane_pool_drain(pool, stage, lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after, wst);
+        plane_pool_drain(pool, stage, lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after, gen, pool_polls,
+                         wst);
         if (lane == 0) {
             solved += wst[0];
             guesses += wst[1];
@@ -1367,19 +1385,20 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after)
+    int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after, uint32_t pool_polls)
 {
     const PlaneIO1 io = {puzzles, sols, status, n};
-    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk, mrv_after);
+    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls);
 }
 
 // several batches, one queue over them (sdk_solve_batches; unordered)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel_multi(
     const PlaneBatches bs, unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack,
-    int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after)
+    int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after,
+    uint32_t pool_polls)
 {
     const PlaneIOn io = {bs};
-    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk, mrv_after);
+    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls);
 }
 
 #endif  // SDK_PLANE_KERNEL_H

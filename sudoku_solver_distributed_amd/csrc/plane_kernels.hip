@@ -35,14 +35,6 @@ static int env_int(const char *name, int dflt)
 // environment's / built-in default)
 static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1}, g_mrv{-1};
 
-int sdk_set_plane_search(int mrv_after)
-{
-    if (mrv_after > (int)plane::MST_PASSES) return -1;
-    const int prev = g_mrv.load();
-    g_mrv = mrv_after < 0 ? -1 : mrv_after;
-    return prev;
-}
-
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 {
     if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 2 || refill == 0 || chunk > PLANE_CHUNK_MAX) return -1;
@@ -59,7 +51,7 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 
 struct PlaneKnobs {
     int refill, tail, tail_mode, chunk;
-    uint32_t mrv_after;
+    uint32_t mrv_after, pool_polls;
 };
 
 static PlaneKnobs plane_knobs(int pipelined)
@@ -80,7 +72,19 @@ static PlaneKnobs plane_knobs(int pipelined)
     chunk = chunk > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : chunk;  // ($SDK_PLANE_CHUNK is not range-checked)
     int mrv = g_mrv >= 0 ? g_mrv.load() : mrv_env;
     mrv = mrv < 0 ? 0 : mrv > (int)plane::MST_PASSES ? (int)plane::MST_PASSES : mrv;
-    return {refill, tail, tail_mode, chunk, (uint32_t)mrv};
+    // flag polls before a pool consumer gives up (~1 s; read at every launch:
+    // tests/test_gpu_full_size.py forces 0 to see the host raise, then
+    // recovers on the same workspace)
+    const uint32_t polls = (uint32_t)env_int("SDK_PLANE_POOL_POLLS", 1 << 23);
+    return {refill, tail, tail_mode, chunk, (uint32_t)mrv, polls};
+}
+
+int sdk_set_plane_search(int mrv_after)
+{
+    if (mrv_after > (int)plane::MST_PASSES) return -2;
+    const int prev = (int)plane_knobs(0).mrv_after;  // the setting in effect, default or not
+    g_mrv = mrv_after < 0 ? -1 : mrv_after;
+    return prev;
 }
 
 hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *status, int64_t n,
@@ -90,7 +94,7 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
     const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);
+                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls);
     return hipGetLastError();
 }
 
@@ -100,7 +104,7 @@ hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws
     const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel_multi, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, bs, ws, stack,
-                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after);
+                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls);
     return hipGetLastError();
 }
 

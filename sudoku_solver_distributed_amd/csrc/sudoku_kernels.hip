@@ -52,6 +52,12 @@ __global__ void arm_kernel(unsigned long long *ws, uint32_t *pool)
     if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
     if (threadIdx.x == WS_DEFER_COUNT) ws[WS_DEFER_COUNT] = 0ull;
     if (threadIdx.x == WS_DEFER_OVER) ws[WS_DEFER_OVER] = 0ull;
+    if (threadIdx.x == WS_GEN) {
+        // the next generation; its low 32 bits (the pool's flag value) never 0
+        unsigned long long g = ws[WS_GEN] + 1ull;
+        if ((uint32_t)g == 0u) g++;
+        ws[WS_GEN] = g;
+    }
 }
 
 #include "packed_solver.h"
@@ -70,6 +76,7 @@ __global__ __launch_bounds__(BLOCK_THREADS, SDK_PACKED_WAVES_PER_EU) void solvep
     const int64_t gw = (int64_t)blockIdx.x * WAVES_PER_BLOCK + (threadIdx.x >> 6);
     const int64_t *best = ordered ? (const int64_t *)&ws[WS_BEST] : nullptr;
 
+    if (gw == 0 && lane == 0) atomicAdd(&ws[WS_ASSIGNED], (unsigned long long)n);  // sdk_verify_workspace
     PCells s;
     pinit_lane(s, lane);
     uint32_t fin = 0, solved = 0, guesses = 0, sweeps = 0;
@@ -505,8 +512,13 @@ static int blocks_per_cu(K kernel, std::atomic<int> &cached)
 }
 static std::atomic<int> g_bpc_packed{0}, g_bpc_plane{0};
 
-// waves of the deferred-board kernels after a plane launch
-static int64_t deferred_waves() { return (int64_t)cu_count(); }
+// waves of the deferred-board kernels after a plane launch: one workgroup
+// (4 waves) per CU.  The count of deferred boards is known only on the
+// device; the waves past it exit at once, and a full grid of them only
+// queues for the slots the next launches in flight want (8.8 % of the
+// traced kernel time), while a batch that is mostly deferred
+// (clashing givens) still gets a wave per SIMD.
+static int64_t deferred_waves() { return (int64_t)cu_count() * WAVES_PER_BLOCK; }
 
 // lanes of a full plane-kernel grid on the current device, and the bytes of
 // their stacks (the workspace holds them after WS_STACK_BYTE)
@@ -635,9 +647,7 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
                              st);
         if (e != hipSuccess) return set_err("sdk_solve_batch: plane launch", e);
         // the boards it left (clashing givens, deep searches): wave per board,
-        // one wave per CU (its waves exit at once when nothing was left, and
-        // a full grid of them only queues for the slots the next launches in
-        // flight want)
+        // one workgroup per CU (deferred_waves)
         const int64_t max_waves = deferred_waves();
         const int64_t groups = (n + 63) / 64;
         const int64_t waves = groups < max_waves ? groups : max_waves;
@@ -807,11 +817,45 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
     out[4] = (int64_t)h[WS_BEST];
     out[5] = (int64_t)h[WS_DEFERRED];
     if (reset) {
-        e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 5 * sizeof(unsigned long long), st);
+        // the counters and the assigned-boards word (never the error word:
+        // only sdk_verify_workspace clears it, once it has reported it)
+        static_assert(WS_ASSIGNED == WS_FINISHED + 5, "counter words");
+        e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 6 * sizeof(unsigned long long), st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return set_err("sdk_read_stats: reset", e);
     }
     return 0;
+}
+
+int sdk_verify_workspace(void *d_workspace, int64_t out[3], void *stream)
+{
+    if (!d_workspace) {
+        snprintf(g_err, sizeof g_err, "sdk_verify_workspace: bad arguments");
+        return -2;
+    }
+    hipStream_t st = (hipStream_t)stream;
+    unsigned long long h[WS_WORDS];
+    hipError_t e = hipMemcpyAsync(h, d_workspace, sizeof h, hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_err("sdk_verify_workspace", e);
+    if (out) {
+        out[0] = (int64_t)h[WS_ASSIGNED];
+        out[1] = (int64_t)h[WS_FINISHED];
+        out[2] = (int64_t)h[WS_ERROR];
+    }
+    if (h[WS_ASSIGNED] == h[WS_FINISHED] && h[WS_ERROR] == 0) return 0;
+    snprintf(g_err, sizeof g_err,
+             "sdk_verify_workspace: %lld boards handed to the solve kernels, %lld answered; error bits 0x%llx%s "
+             "(pool slot %llu)",
+             (long long)h[WS_ASSIGNED], (long long)h[WS_FINISHED], h[WS_ERROR],
+             (h[WS_ERROR] & SDK_ERR_POOL_WAIT) ? ": a tail-pool record was never published" : "", h[WS_ERR_SLOT]);
+    // reported once: the next check starts from a consistent workspace
+    unsigned long long fix[2] = {h[WS_FINISHED], 0ull};
+    static_assert(WS_ERROR == WS_ASSIGNED + 1, "assigned / error words");
+    e = hipMemcpyAsync((unsigned long long *)d_workspace + WS_ASSIGNED, fix, sizeof fix, hipMemcpyHostToDevice, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_err("sdk_verify_workspace: clear", e);
+    return -3;
 }
 
 __global__ void snapshot_stats_kernel(const unsigned long long *__restrict__ ws, int64_t *__restrict__ out)

@@ -63,7 +63,7 @@ from typing import List, Optional
 
 import torch
 
-from .solver import SDK_NO_RETURN, SDK_SOLVED, BatchSolver, as_boards, get_solver
+from .solver import SDK_NO_RETURN, SDK_SOLVED, BatchSolver, SudokuHipError, as_boards, get_solver
 
 logger = logging.getLogger(__name__)
 
@@ -143,6 +143,13 @@ class GpuSolverBackend:
                     events.append(ev)
             for ev in events:
                 ev.synchronize()
+        # every board of the batch answered: the stream-ordered count of
+        # finished boards around each solver's launch equals its share
+        for i in range(k):
+            want = (i + 1) * n // k - i * n // k
+            if want and int(counts[i, 0]) != want:
+                raise SudokuHipError(f"solver {i}: {int(counts[i, 0])} of {want} boards answered "
+                                     f"({self.solvers[i].verify()})")
         return out, st, int(counts[:, 3].sum())
 
     def peer_solve(self, boards: torch.Tensor):

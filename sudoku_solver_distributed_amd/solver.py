@@ -449,6 +449,29 @@ class BatchSolver:
         return {"finished": out[0], "solved": out[1], "guesses": out[2], "sweeps": out[3], "best": out[4],
                 "deferred": out[5]}
 
+    def verify(self, stream=None) -> dict:
+        """Every board handed to this workspace's solve kernels since the last
+        stats(reset=True) has its answer, and no kernel reported an error
+        (sdk_verify_workspace; synchronises the stream).  Returns {"assigned",
+        "finished", "error"}; raises SudokuHipError otherwise -- a board a
+        kernel took but could not finish (a tail-pool record never published,
+        DESIGN.md §3) is never a silent stale output."""
+        out = (ctypes.c_int64 * 3)()
+        with self._lock, torch.cuda.device(self.device):
+            rc = self.lib.sdk_verify_workspace(self.workspace.data_ptr(), out, self._ws_stream(stream))
+        if rc == -3:
+            raise SudokuHipError(self.lib.sdk_last_error().decode(errors="replace"))
+        _lib.check(rc, "sdk_verify_workspace")
+        return {"assigned": out[0], "finished": out[1], "error": out[2]}
+
+    def verify_inflight(self) -> dict:
+        """verify() over the solve_inflight slots' workspaces (summed)."""
+        tot = {"assigned": 0, "finished": 0, "error": 0}
+        for solver, s in (self._slots or [(self, None)]):
+            for k, v in solver.verify(stream=s).items():
+                tot[k] += v
+        return tot
+
     def stats_snapshot(self, stream=None) -> torch.Tensor:
         """The counters of stats() as a device int64 (6,) tensor, copied
         asynchronously in stream order with this workspace's solves

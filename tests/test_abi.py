@@ -134,18 +134,27 @@ def test_plane_tuning_rejects_oversized_chunks():
 
 
 def test_plane_search_knob_range():
-    """sdk_set_plane_search: the previous setting back (-1 = default),
-    out-of-range values refused.  Host-side only."""
+    """sdk_set_plane_search: the setting in effect before the call back (the
+    default's value, 64, when nothing overrode it), out-of-range values
+    refused with -2 and nothing changed.  Host-side only."""
     from sudoku_solver_distributed_amd import _lib
     L = _lib.load()
     try:
         L.sdk_set_plane_search(-1)
-        assert L.sdk_set_plane_search(64) == -1
-        assert L.sdk_set_plane_search(0) == 64
-        assert L.sdk_set_plane_search(1 << 24) == -1
+        assert L.sdk_set_plane_search(48) == 64
+        assert L.sdk_set_plane_search(0) == 48
+        assert L.sdk_set_plane_search(1 << 24) == -2
         assert L.sdk_set_plane_search(-1) == 0
+        assert L.sdk_set_plane_search(-1) == 64
     finally:
         L.sdk_set_plane_search(-1)
+
+
+def test_verify_workspace_arguments():
+    """sdk_verify_workspace refuses a null workspace (-2) without a GPU."""
+    from sudoku_solver_distributed_amd import _lib
+    L = _lib.load()
+    assert L.sdk_verify_workspace(None, None, None) == -2
 
 
 def test_pipelined_launch_choice():
