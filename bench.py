@@ -11,7 +11,7 @@ across 1/2/4/8 MI355X"): B boards per step over ALL ranks, rank r solving
 its shard_bounds share (B/N boards) of every step's batch; weak: B boards per
 GPU per step.  A shard of a step too small to fill the GPU alone (2^17 boards
 at N = 8) is launched together with the rank's next steps' shards --
-sdk_solve_batches, one queue over up to 16 batches that drains once -- until a
+sdk_solve_batches, one queue over up to 32 batches that drains once -- until a
 launch holds --launch-boards (2^20) boards; each step's shard keeps its own
 input and output buffers.  Consecutive launches keep --inflight (default 6,
 with $GPU_MAX_HW_QUEUES = 8 set below) in flight per GPU, each on its own
@@ -256,7 +256,7 @@ def shard_rates(solver, boards, launch_boards: int = 1 << 21, reps: int = 3):
         res = {"boards_per_step": sh, "steps": k}
         from sudoku_solver_distributed_amd.solver import default_inflight
         m = default_inflight()[0]
-        for name, g in (("ungrouped", 1), ("grouped", max(1, min(16, -(-launch_boards // sh))))):
+        for name, g in (("ungrouped", 1), ("grouped", max(1, min(32, -(-launch_boards // sh))))):
             nb = m * max(g, div)
             bufs = [(torch.empty_like(parts[0]), torch.empty(sh, dtype=torch.int32, device=boards.device))
                     for _ in range(nb)]
@@ -364,9 +364,17 @@ def main():
                     help="strong: --batch boards per step sharded over the ranks (BASELINE configs[2]); "
                          "weak: --batch boards per GPU per step")
     ap.add_argument("--launch-boards", type=int, default=-1,
-                    help="a launch solves consecutive steps' shards together (sdk_solve_batches, <= 16 steps) "
+                    help="a launch solves consecutive steps' shards together (sdk_solve_batches, <= 32 steps) "
                          "until it holds this many boards; 0 = one step per launch; -1: 2^21 when a rank's "
                          "shard is below 2^20 boards (strong scaling, N > 1), else one step per launch")
+    ap.add_argument("--plan", choices=("run", "inflight"), default="run",
+                    help="run (default): the timed steps as few launches as sdk_solve_batches allows (<= 32 steps "
+                         "each), each on a full grid, the next queued behind the current one -- one drain per "
+                         "launch, one launch for K <= 32; inflight: round 4's plan, one step (or --launch-boards "
+                         "boards of steps) per launch, --inflight launches kept in flight at --grid-waves each")
+    ap.add_argument("--launches", type=int, default=0,
+                    help="split the timed steps' shards into this many launches of equal step counts "
+                         "(sdk_solve_batches, <= SDK_MAX_BATCHES steps each) instead of --launch-boards")
     ap.add_argument("--seed", type=int, default=2024)
     ap.add_argument("--workload", choices=("hard17", "hard_search"), default="hard17",
                     help="timed boards: BASELINE's hard 17-clue set (default, the metric's config) or the "
@@ -453,8 +461,16 @@ def main():
     # Sharded steps (N > 1) go 2^21 boards to a launch at 2 waves per SIMD:
     # fewer launches, so fewer drains at the end of the run (one rank of
     # N = 2 / 4 / 8 at 20 steps: +6 / +6 / +5 % over 2^20 at 1 wave)
+    from sudoku_solver_distributed_amd._lib import SDK_MAX_BATCHES
     launch_boards = args.launch_boards if args.launch_boards >= 0 else (1 << 21 if shard < (1 << 20) else 0)
-    group = 1 if launch_boards <= shard else min(16, -(-launch_boards // shard))
+    group = 1 if launch_boards <= shard else min(SDK_MAX_BATCHES, -(-launch_boards // shard))
+    plan_run = args.plan == "run" and args.launches <= 0 and args.launch_boards < 0
+    if plan_run:
+        # the whole run's steps in ceil(K / 32) launches of equal step counts
+        n_launch = -(-args.steps // SDK_MAX_BATCHES)
+        group = -(-args.steps // n_launch)
+    if args.launches > 0:
+        group = min(SDK_MAX_BATCHES, -(-args.steps // args.launches))
     # one input per step of a launch group (each step its own boards): step
     # j's batch is the synthetic batch rotated by 7919 j boards (one
     # generation however many steps a launch holds); strong: this rank's
@@ -469,6 +485,8 @@ def main():
     from sudoku_solver_distributed_amd.solver import default_inflight
     m_def, gw_def = default_inflight()
     m = m_def if args.inflight < 0 else max(1, args.inflight)
+    if plan_run and args.inflight < 0:
+        m = 2  # the running launch and the next one queued behind it
     # one (solutions, status) pair per step that can be in flight: step i
     # reads inputs[i % group] and writes pair i % (m * group)
     nb = m * group
@@ -478,7 +496,7 @@ def main():
     solver._slot_solvers(m)  # slot workspaces allocated before any timing
     if args.grid_waves >= 0:
         grid_waves = args.grid_waves
-    elif m == 1:
+    elif m == 1 or plan_run:
         grid_waves = 0
     elif group > 1 and args.inflight < 0:
         grid_waves = GRID_WAVES_GROUPED
@@ -486,11 +504,16 @@ def main():
         grid_waves = gw_def if args.inflight < 0 else (1 if m >= 5 else 2)
     grid_waves_used = grid_waves
 
+    # the launches that share their tails through the XCD pool (unpipelined):
+    # plan run: the last (nothing is queued behind it); inflight: half the
+    # launches in flight (solve_inflight's default)
+    pool_last_arg = args.pool_last if args.pool_last >= 0 else (1 if plan_run else None)
+
     def steps(k, events=None, inflight=m):
         solver.solve_inflight([inputs[i % group] for i in range(k)], [bufs[i % nb][0] for i in range(k)],
                               [bufs[i % nb][1] for i in range(k)], inflight=inflight, launch_events=events,
                               grid_waves=grid_waves if inflight > 1 else 0, group=group,
-                              pool_last=None if args.pool_last < 0 else args.pool_last)
+                              pool_last=pool_last_arg)
 
     steps(args.warmup)
     torch.cuda.synchronize(dev)
@@ -571,7 +594,7 @@ def main():
     kern_s = kern_ms / 1e3  # this GPU's share of the timed region per step
     # pool_last: the launches at the end that share their tails through the
     # XCD pool (solve_inflight's default: half the launches in flight; -1 all)
-    pool_last = args.pool_last if args.pool_last >= 0 else ((m + 1) // 2 if m > 1 else -1)
+    pool_last = pool_last_arg if pool_last_arg is not None else ((m + 1) // 2 if m > 1 else -1)
     # (hw_queues: the process's hardware queues, which decide whether the
     # launches in flight run side by side -- bench.py sets 8, HIP's default is 4)
     shape = {"boards_per_step": shard, "group": group, "inflight": m, "grid_waves": grid_waves_used,

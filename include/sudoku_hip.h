@@ -93,7 +93,7 @@ int sdk_solve_batch_grid(const uint8_t *d_puzzles, uint8_t *d_solutions, int32_t
  * overlap each other's outputs.  Returns 0 / -1 (HIP error) / -2 (bad
  * arguments).  Replaces the same reference walks as sdk_solve_batch
  * (gen.py:6-28, node.py:62-74), once per board. */
-#define SDK_MAX_BATCHES 16
+#define SDK_MAX_BATCHES 32
 int sdk_solve_batches(const uint8_t *const *d_puzzles, uint8_t *const *d_solutions, int32_t *const *d_status,
                       const int64_t *n, int count, void *d_workspace, int order, void *stream, int grid_waves);
 

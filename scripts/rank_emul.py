@@ -39,6 +39,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=1)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--ranks", default="all", help="ranks to run per world (comma list; 'all': every rank)")
+    ap.add_argument("--label", default="")
     args, extra = ap.parse_known_args()
     batch = 1 << 20
     for a, b in zip(extra, extra[1:]):
@@ -49,7 +51,8 @@ def main():
     for rnd in range(args.rounds):
         for w in (int(x) for x in args.worlds.split(",")):
             ranks = []
-            for r in range(w):
+            rlist = range(w) if args.ranks == "all" else [int(x) for x in args.ranks.split(",") if int(x) < w]
+            for r in rlist:
                 t0 = time.time()
                 line = run_rank(w, r, args.steps, args.warmup, extra)
                 wall = line["ms_per_step"] * args.steps / 1e3
@@ -61,7 +64,7 @@ def main():
             job = batch * args.steps / slow
             if w == 1:
                 base = job
-            rec = {"world": w, "round": rnd, "steps": args.steps, "max_rank_wall_s": slow,
+            rec = {"label": args.label, "flags": extra, "world": w, "round": rnd, "steps": args.steps, "max_rank_wall_s": slow,
                    "min_rank_wall_s": min(x["wall_s"] for x in ranks),
                    "job_boards_per_s": job, "x_of_1gpu": job / base if base else None,
                    "efficiency": job / base / w if base else None, "ranks": ranks}

@@ -45,7 +45,7 @@ EXPORTS = (
     "sdk_set_plane_search",
 )
 SDK_KERNELS = {"auto": 1, "packed": 5, "plane": 6}
-SDK_MAX_BATCHES = 16  # sdk_solve_batches: batches per launch
+SDK_MAX_BATCHES = 32  # sdk_solve_batches: batches per launch
 SDK_GRID_PIPELINED = 0x10000  # grid_waves flag: another launch is queued behind this one
 # device symbol of each solve kernel (rocprofv3 Kernel_Name, profiles/pmc_<symbol>.json)
 KERNEL_SYMBOLS = {1: "plane_kernel", 5: "solvep_kernel", 6: "plane_kernel"}

@@ -82,7 +82,7 @@ __device__ __forceinline__ int order_cell(uint64_t eb0, uint64_t eb1, int order)
 // Several batches in one plane launch (sdk_solve_batches): the queue hands
 // out virtual indices over the batches laid end to end; a lane's board id is
 // batch j << PLANE_BATCH_SHIFT | index in batch j (deferred-list entries too).
-// Passed by value as a kernel argument (520 bytes).
+// Passed by value as a kernel argument (1032 bytes at 32 batches).
 struct PlaneBatches {
     int64_t end[SDK_MAX_BATCHES];  // virtual index one past batch j (cumulative, ascending)
     const uint8_t *in[SDK_MAX_BATCHES];

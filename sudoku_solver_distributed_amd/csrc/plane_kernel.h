@@ -269,7 +269,7 @@ struct PlaneIOn {
     static constexpr bool multi = true;
     const PlaneBatches &b;
     __device__ __forceinline__ int64_t total() const { return b.end[b.count - 1]; }
-    // batch of virtual v (wave-uniform: a scalar loop over at most 15 bounds)
+    // batch of virtual v (wave-uniform: a scalar loop over at most 31 bounds)
     __device__ __forceinline__ int batch(int64_t v) const
     {
         int j = 0;

@@ -189,7 +189,7 @@ class BatchSolver:
         batches laid end to end and drains once, so batches too small to fill
         the GPU on their own (a multi-GPU shard of one step) keep every lane
         busy.  Each batch's outputs are exactly solve()'s.  At most
-        SDK_MAX_BATCHES (16) batches; unordered only."""
+        SDK_MAX_BATCHES (32) batches; unordered only."""
         if not (len(batches) == len(outs) == len(statuses)) or not 1 <= len(batches) <= _lib.SDK_MAX_BATCHES:
             raise ValueError(f"1..{_lib.SDK_MAX_BATCHES} batches, one out and one status tensor each")
         ps = [self._dev(as_boards(b)) for b in batches]

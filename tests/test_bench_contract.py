@@ -4,32 +4,41 @@ bench line's roofline.achieved / frac would silently be null."""
 import json
 import os
 
+import pytest
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def test_default_kernel_has_matching_pmc_profile():
-    from sudoku_solver_distributed_amd import _lib
-    kname = _lib.KERNEL_SYMBOLS[_lib.SDK_KERNELS["auto"]]
-    path = os.path.join(ROOT, "profiles", f"pmc_{kname}.json")
-    assert os.path.exists(path), path
-    with open(path) as f:
-        pmc = json.load(f)
-    # bench.py defaults at N = 1: --batch 2^20 boards per step, --seed 2024,
-    # one step per launch, 6 launches in flight at 1 wave per SIMD -- the
-    # counters must come from the launch shape the bench times (bench.py
-    # nulls roofline.frac / traffic otherwise)
-    # (bench.py sets GPU_MAX_HW_QUEUES = 8 before HIP starts)
-    from unittest import mock
-    from sudoku_solver_distributed_amd.solver import default_inflight
-    with mock.patch.dict(os.environ, {"GPU_MAX_HW_QUEUES": "8"}):
-        inflight, grid_waves = default_inflight()
-    assert pmc["kernel"] == kname
-    assert pmc["seed"] == 2024 and pmc.get("workload", "hard17") == "hard17"
-    assert pmc["shape"] == {"boards_per_step": 1 << 20, "group": 1, "inflight": inflight, "grid_waves": grid_waves,
-                            "pool_last": (inflight + 1) // 2}
-    assert pmc["counters_per_launch"]["SQ_WAVES"] == 256 * 4 * grid_waves
-    assert pmc["valu_insts_per_launch"] > 0
-    assert pmc["hbm_bytes_per_launch"] is None or pmc["hbm_bytes_per_launch"] > 0
+def bench_shape(world, steps=20):
+    """The launch shape bench.py's default plan gives one rank of a
+    strong-scaling job of `world` ranks at the driver's --steps 20 (plan
+    "run": the 20 steps' shards as one sdk_solve_batches launch on a full
+    grid; bench.py sets GPU_MAX_HW_QUEUES = 8 before HIP starts)."""
+    from sudoku_solver_distributed_amd._lib import SDK_MAX_BATCHES
+    n_launch = -(-steps // SDK_MAX_BATCHES)
+    return {"boards_per_step": (1 << 20) // world, "group": -(-steps // n_launch), "inflight": 2, "grid_waves": 0,
+            "pool_last": 1, "hw_queues": 8}
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_default_shapes_have_matching_pmc_profiles(world):
+    """For the driver's 1 / 2 / 4 / 8-GPU runs (--steps 20) a committed PMC
+    summary of exactly that rank's launch shape exists (bench.py picks it by
+    shape), so every scaling line carries roofline.frac and traffic."""
+    import glob
+    kname = "plane_kernel_multi"   # a multi-step launch (sdk_solve_batches)
+    want = bench_shape(world)
+    found = []
+    for path in glob.glob(os.path.join(ROOT, "profiles", f"pmc_{kname}*.json")):
+        with open(path) as f:
+            pmc = json.load(f)
+        if (pmc.get("kernel") == kname and pmc.get("seed") == 2024 and pmc.get("workload", "hard17") == "hard17"
+                and pmc.get("shape") == want):
+            found.append(pmc)
+    assert found, (world, want)
+    pmc = found[0]
+    assert pmc["valu_insts_per_step"] > 0 and pmc["steps"] == 20
+    assert pmc.get("hbm_bytes_per_step") is None or pmc["hbm_bytes_per_step"] > 0
 
 
 def _free_port():
@@ -37,9 +46,6 @@ def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
-
-
-import pytest  # noqa: E402
 
 
 @pytest.mark.gpu
@@ -74,11 +80,10 @@ def test_bench_two_rank_path_runs():
     assert len(lines) == 1 and not [l for l in outs[1].splitlines() if l.startswith("{")]
     d = json.loads(lines[0])
     # strong scaling (the default): the 2^20-board step split over the two
-    # ranks, each rank's launches holding 2^21 boards (four steps' shards) at
-    # 2 waves per SIMD
+    # ranks, each rank's two timed steps one launch on a full grid (plan run)
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["dist_backend"] == "gloo"
     assert d["config"]["global_batch"] == 1 << 20 and d["config"]["boards_per_gpu_per_step"] == 1 << 19
-    assert d["config"]["steps_per_launch"] == 4 and d["roofline"]["kernel"] == "plane_kernel_multi"
-    assert d["config"]["grid_waves_per_simd"] == 2
+    assert d["config"]["steps_per_launch"] == 2 and d["roofline"]["kernel"] == "plane_kernel_multi"
+    assert d["config"]["grid_waves_per_simd"] is None
     assert d["side_configs"]["pathological"]["ranks"] == 2 and d["side_configs"]["pathological"]["identical"]
     assert d["all_solved_and_checked"] and d["value"] > 0

@@ -109,11 +109,11 @@ def test_solve_inflight_grouped(solver):
     for (ws, wt), (gs, gt) in zip(want, got):
         assert torch.equal(ws, gs) and torch.equal(wt, gt)
     with pytest.raises(ValueError):
-        solver.solve_inflight(steps, outs, sts, group=17)
+        solver.solve_inflight(steps, outs, sts, group=33)
     with pytest.raises(ValueError):
         solver.solve_inflight(steps, outs, sts, group=2, ordered=True)
     with pytest.raises(ValueError):
-        solver.solve_batches(steps[:1] * 17, outs[:1] * 17, sts[:1] * 17)
+        solver.solve_batches(steps[:1] * 33, outs[:1] * 33, sts[:1] * 33)
 
 
 @pytest.mark.parametrize("order", ["gen", "node"])
