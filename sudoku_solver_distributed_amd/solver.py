@@ -456,17 +456,17 @@ class BatchSolver:
         "finished", "error"}; raises SudokuHipError otherwise -- a board a
         kernel took but could not finish (a tail-pool record never published,
         DESIGN.md §3) is never a silent stale output."""
-        out = (ctypes.c_int64 * 3)()
+        out = (ctypes.c_int64 * 4)()
         with self._lock, torch.cuda.device(self.device):
             rc = self.lib.sdk_verify_workspace(self.workspace.data_ptr(), out, self._ws_stream(stream))
         if rc == -3:
             raise SudokuHipError(self.lib.sdk_last_error().decode(errors="replace"))
         _lib.check(rc, "sdk_verify_workspace")
-        return {"assigned": out[0], "finished": out[1], "error": out[2]}
+        return {"assigned": out[0], "finished": out[1], "error": out[2], "splits": out[3]}
 
     def verify_inflight(self) -> dict:
         """verify() over the solve_inflight slots' workspaces (summed)."""
-        tot = {"assigned": 0, "finished": 0, "error": 0}
+        tot = {"assigned": 0, "finished": 0, "error": 0, "splits": 0}
         for solver, s in (self._slots or [(self, None)]):
             for k, v in solver.verify(stream=s).items():
                 tot[k] += v
