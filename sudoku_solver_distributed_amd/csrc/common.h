@@ -40,6 +40,7 @@ enum {
 // WS_ERROR bits
 #define SDK_ERR_POOL_WAIT 1u  // a pool consumer gave up waiting on a claimed record: that board was not solved
 #define SDK_ERR_POOL_IDLE 2u  // waves waited ~0.25 s for a count-mode board to deal out work (a counting leak)
+#define SDK_ERR_QUAD_STALL 4u // the four-board tail solver ran ~4 M passes without finishing (a search bug)
 
 __device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
 

@@ -1026,6 +1026,7 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
 }
 
 // ---- the tail pool on the four-board solver (tail mode 3, plane_quad.h)
+enum { Q_SEARCHING = -100 };  // a row's answer while it has none (wide::W_* are -1..3)
 // Claim one published record (wave-uniform): 1 and its slot in h, 0 if none
 // is published, -1 if its flag never came (SDK_ERR_POOL_WAIT set).
 __device__ __forceinline__ int pool_claim(const PlanePool &pool, unsigned long long *__restrict__ ws, uint32_t gen,
@@ -1113,7 +1114,16 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
     auto ld_entry = [&](uint32_t level) {
         return __builtin_amdgcn_raw_buffer_load_b32(stack_rsrc, (int)(sbase + level * 128u + 108u), 0, 0);
     };
-    for (;;) {
+    for (uint32_t guard = 0;; ++guard) {
+        if (guard > (1u << 22)) {  // ~4 M passes: no board needs that; leave loudly rather than hang
+            if (lane == 0) atomicOr(&ws[WS_ERROR], (unsigned long long)SDK_ERR_QUAD_STALL);
+            if (lane < 4) {  // diagnostic: each row's state
+                const int l = 16 * lane;
+                ws[16 + 2 * lane] = ((unsigned long long)rdlane(mst, l) << 32) | rdlane(depth, l);
+                ws[17 + 2 * lane] = ((unsigned long long)rdlane((uint32_t)busy, l) << 32) | rdlane(und[0] | und[1] | und[2], l);
+            }
+            break;
+        }
         // ---- refill the idle rows from the pool (other waves may still publish)
         uint64_t bm = __builtin_amdgcn_ballot_w64(busy);
         if (pool_empty && (++iter & 7u) == 0u) pool_empty = false;
@@ -1163,7 +1173,7 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
         int r = busy ? (int)r0 : quad::OPEN;
         mst += busy ? 1u : 0u;
         int mode = plane::mst_mode(mst);
-        int res = -1;          // the row's answer (wide::W_*), -1: searching
+        int res = Q_SEARCHING;  // the row's answer (wide::W_*; W_OVERFLOW is -1)
         int reload = -1;       // a level whose planes replace the row's board
         bool scan = false;     // reload scans down for an untried digit
         bool guess = false, push_sol = false;
@@ -1220,6 +1230,8 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
         uint32_t cand = 0;
         const uint64_t gm = __builtin_amdgcn_ballot_w64(guess);
         if (gm) {
+            // (the picks only in the guessing rows: they take ctz / clz of
+            // undetermined-cell words, which are 0 in a solved row)
             if (__builtin_amdgcn_ballot_w64(guess && mode == plane::M_COUNT)) {
                 uint32_t e2[3], e3[3];
 #pragma unroll
@@ -1229,9 +1241,9 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
                     e2[b] = und[b] & plane::andn(t, th);
                     e3[b] = und[b] & plane::andn(th, f);
                 }
-                if (mode == plane::M_COUNT) plane::pick_mrv_masks(e2, e3, und, band, pos);
-                else plane::pick_cell(und, node_order, band, pos);
-            } else {
+                if (guess && mode == plane::M_COUNT) plane::pick_mrv_masks(e2, e3, und, band, pos);
+                else if (guess) plane::pick_cell(und, node_order, band, pos);
+            } else if (guess) {
                 plane::pick_cell(und, node_order, band, pos);
             }
             const uint32_t wb = band == 0 ? w[0] : band == 1 ? w[1] : w[2];
@@ -1279,7 +1291,7 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
                 reload--;
             }
         }
-        if (guess && res < 0) {
+        if (guess && res == Q_SEARCHING) {
             depth++;
             bguess++;
             if (dg == 0u) n_guess++;
@@ -1291,7 +1303,7 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
             }
         }
         // ---- rows with an answer write it and take the next board
-        const uint64_t dm = __builtin_amdgcn_ballot_w64(busy && res >= 0);
+        const uint64_t dm = __builtin_amdgcn_ballot_w64(busy && res != Q_SEARCHING);
         if (dm) {
             for (uint32_t q = 0; q < 4u; ++q) {
                 if (!((dm >> (16u * q)) & 1u)) continue;
@@ -1307,7 +1319,7 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
                                     (int64_t)rdlane((uint32_t)pb, (int)(16u * q));
                 plane_wide_answer(qres, ww, qpb, rdlane(bguess, (int)(16u * q)), lane, WL, io, ws, defer_list, best, st);
             }
-            if (busy && res >= 0) busy = false;
+            if (busy && res != Q_SEARCHING) busy = false;
         }
     }
     st[2] += wave_sum(n_pass);
