@@ -1,16 +1,20 @@
 """Per-launch figures of the plane kernel from a rocprofv3 kernel trace of a
-bench.py run (--kernel-trace ... -o run --output-format csv), for checking
-the bench line's roofline.kernel_ms: launches that overlap their
-predecessor (two in flight) form the timed region, whose span / launches is
-kernel_ms; launches that do not are the back-to-back `serial` steps.
+bench.py run (--kernel-trace ... -o run --output-format csv), to check the
+bench line's roofline.kernel_ms.  Plan "run" (bench.py's default): the
+warm-up steps are one launch and the K timed steps one more (K <= 32), so
+the timed launch is the longest plane launch and kernel_ms = its span / K.
+Launches that overlap their predecessor (plan "inflight") form one region.
 
-    python scripts/trace_summary.py gpurun_out/prof_trace/run_kernel_trace.csv [out.json]
+    python scripts/trace_summary.py gpurun_out/prof_trace/run_kernel_trace.csv [out.json] [--steps K]
 """
 import csv
 import json
 import sys
 
-rows = [r for r in csv.DictReader(open(sys.argv[1])) if r["Kernel_Name"].startswith("plane_kernel")]
+args = [a for a in sys.argv[1:] if not a.startswith("--")]
+steps = int(sys.argv[sys.argv.index("--steps") + 1]) if "--steps" in sys.argv else 20
+args = [a for a in args if a != str(steps)] if "--steps" in sys.argv else args
+rows = [r for r in csv.DictReader(open(args[0])) if r["Kernel_Name"].startswith("plane_kernel")]
 rows.sort(key=lambda r: int(r["Start_Timestamp"]))
 st = [int(r["Start_Timestamp"]) for r in rows]
 en = [int(r["End_Timestamp"]) for r in rows]
@@ -23,18 +27,17 @@ for i in range(1, len(rows)):
         runs.append(cur)
         cur = [i]
 runs.append(cur)
-inflight = max(runs, key=len)
-region_ms = (max(en[i] for i in inflight) - st[inflight[0]]) / 1e6
-serial = [i for r in runs if len(r) == 1 for i in r]
+spans = [(max(en[i] for i in r) - st[r[0]]) / 1e6 for r in runs]
+timed = max(range(len(runs)), key=lambda k: spans[k])
 out = {
-    "trace": sys.argv[1],
+    "trace": args[0],
+    "kernel": rows[runs[timed][0]]["Kernel_Name"].split("(")[0],
     "launches": len(rows),
-    "inflight": {"launches": len(inflight), "region_ms_per_launch": region_ms / len(inflight),
-                 "mean_span_ms": sum(en[i] - st[i] for i in inflight) / len(inflight) / 1e6},
-    "serial": {"launches": len(serial),
-               "mean_span_ms": sum(en[i] - st[i] for i in serial) / max(len(serial), 1) / 1e6},
+    "regions_ms": spans,
+    "timed": {"launches": len(runs[timed]), "region_ms": spans[timed], "steps": steps,
+              "region_ms_per_step": spans[timed] / steps},
 }
 print(json.dumps(out, indent=1))
-if len(sys.argv) > 2:
-    with open(sys.argv[2], "w") as f:
+if len(args) > 1:
+    with open(args[1], "w") as f:
         json.dump(out, f, indent=1)

@@ -646,7 +646,11 @@ __device__ __forceinline__ void plane_wide_answer(int r, uint32_t w, int64_t pb,
 #endif
 // (the waiting waves poll COUNTING / HUNGRY: a line of their own, so the
 // polls do not queue in front of the claims' atomics on the first one)
-enum { POOL_RESERVED = 0, POOL_AVAIL = 1, POOL_HEAD = 2, POOL_DESC_NEXT = 3, POOL_COUNTING = 32, POOL_HUNGRY = 33 };
+enum {
+    POOL_RESERVED = 0, POOL_AVAIL = 1, POOL_HEAD = 2, POOL_DESC_NEXT = 3,
+    POOL_COUNTING = 32, POOL_HUNGRY = 33,
+    POOL_LANE_LIVE = 34  // waves still in their lane loop (policy 4: they may hand boards over)
+};
 static_assert(POOL_DESC_NEXT < 4 && POOL_HUNGRY < 36, "pool control words re-armed per call (arm_kernel)");
 // descriptor words: subtrees outstanding, completions, walk needed, board id
 // lo / hi; the first completion's planes at DESC_FOUND + 3d+b, the root's at
@@ -743,7 +747,7 @@ struct PoolHook {
     __device__ __forceinline__ void try_split(uint32_t w, uint32_t depth, uint32_t &mst, const Stack &stk,
                                               const wide::Lanes &L)
     {
-        if (!mode || mode == 3 || depth == 0 || (looks >> 31)) return;  // (3: diagnostic, waves wait, no deals)
+        if (!mode || mode >= 3 || depth == 0 || (looks >> 31)) return;  // (3, 4: waves wait, no deals)
         if (mode == 1) {
             if ((++looks % SDK_PLANE_SPLIT_EVERY) != 0u) return;
             if (pool_load(pool.word(POOL_HUNGRY)) <= 0) return;
@@ -873,8 +877,10 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
         if (pool_load(pool.word(POOL_AVAIL)) <= 0) {
             // nothing published: wait only while a count-mode board is being
             // solved from the pool (it may deal out subtrees)
-            if (!split || pool_load(pool.word(POOL_COUNTING)) <= 0) break;
-            if (++idle > (1u << 17)) {
+            if (!split || (pool_load(pool.word(POOL_COUNTING)) <= 0 &&
+                           (split != 4 || pool_load(pool.word(POOL_LANE_LIVE)) <= 0)))
+                break;
+            if (++idle > (1u << 13)) {
                 // ~0.25 s: no board takes that long; a leaked count would hang
                 // the launch, so leave (every record is still taken: a
                 // publishing wave drains its own before it exits) and say so
@@ -885,7 +891,9 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
                 pool_add(pool.word(POOL_HUNGRY), 1);
                 waiting = true;
             }
-            __builtin_amdgcn_s_sleep(64);
+            // back off: 1.7 us doubling to ~27 us between polls (a wave's
+            // polls must not crowd the L2 channel the solving waves use)
+            for (uint32_t k = 0; k < (1u << (idle < 4 ? idle : 4)); ++k) __builtin_amdgcn_s_sleep(64);
             continue;
         }
         uint32_t h = 0;
@@ -1393,6 +1401,11 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     bool queue_out = false;
     const int64_t nwaves = (int64_t)gridDim.x * (PLANE_THREADS / 64);
     uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
+    // split policy 4 (steal): this wave counts in its XCD pool's lane-loop waves
+    const bool steal_on = split == 4 && tail_mode >= 2 && !ordered;
+    const PlanePool steal_pool = plane_pool(defer_list);
+    uint32_t steal_chk = 0;
+    if (steal_on) pool_add(steal_pool.word(POOL_LANE_LIVE), 1);
 #if SDK_PLANE_STAMPS
     const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t st_t1 = 0;
@@ -1763,7 +1776,11 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             // wave-per-board solver (packed_solver.h) -- and exits.
             if (drained && tail > 0) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                if (act && __builtin_popcountll(act) <= tail) {
+                // policy 4: while waves of the XCD wait in the pool, hand over
+                // as many boards as the tail records hold (looked at every 8th time)
+                const bool steal = steal_on && act && __builtin_popcountll(act) <= PLANE_TAIL_MAX &&
+                                   (++steal_chk & 7u) == 0u && pool_load(steal_pool.word(POOL_HUNGRY)) > 0;
+                if (act && (__builtin_popcountll(act) <= tail || steal)) {
                     if (state == PL_ACTIVE && !tail_mode) guesses -= bguess;  // those searches start over
                     tail_act = act;
                     break;
@@ -1817,6 +1834,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         }
     }
     if (ob_count) plane_flush_outbox(outbox, ob_count, lane, io);
+    if (steal_on) pool_add(steal_pool.word(POOL_LANE_LIVE), -1);
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
     const uint64_t st_t3 = __builtin_amdgcn_s_memrealtime();  // the lane loop ended

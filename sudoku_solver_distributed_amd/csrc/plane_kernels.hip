@@ -80,7 +80,7 @@ static PlaneKnobs plane_knobs(int pipelined)
     // split counting in the tail pool (plane_kernel.h): 0 off, 1 while waves
     // wait for work, 2 at every chance (tests); read at every launch
     int split = env_int("SDK_PLANE_SPLIT", SDK_PLANE_SPLIT);
-    split = split < 0 ? 0 : split > 3 ? 3 : split;
+    split = split < 0 ? 0 : split > 4 ? 4 : split;
     return {refill, tail, tail_mode, chunk, (uint32_t)mrv, polls, split};
 }
 
