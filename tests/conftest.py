@@ -37,3 +37,18 @@ def grid9(s):
 def solver():
     from sudoku_solver_distributed_amd.solver import get_solver
     return get_solver()
+
+
+@pytest.fixture(autouse=True)
+def _every_board_answered(request):
+    """After every test that used the session solver: every board its solve
+    kernels took since the last stats reset was answered and no kernel set an
+    error bit (sdk_verify_workspace), on its own workspace and on the
+    solve_inflight slots' -- the no-silent-drop contract, suite-wide."""
+    yield
+    if "solver" not in request.fixturenames:
+        return
+    s = request.getfixturevalue("solver")
+    s.verify()
+    if s._slots:
+        s.verify_inflight()
