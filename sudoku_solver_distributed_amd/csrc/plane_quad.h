@@ -115,6 +115,9 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
 
     // ---- C: places of this lane's digit per row / box of each band, per column over the bands
     V oc[3], tc[3], gr[3], hb[3];
+#if SDK_PLANE_LC
+    V vp[3];
+#endif
     V rowall = V(GUARDS), boxall = V(BOXC);
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
@@ -131,7 +134,11 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
         const V ob = wide::or3(oc[b], o1, o2);
         boxall = boxall & ob;
         const V tb = wide::or3(tc[b], tc[b] >> 1, tc[b] >> 2);
-        hb[b] = wide::mul24(wide::andn2(ob, tb, wide::maj3(oc[b], o1, o2)) & BOXC, 0x701C07u);  // boxes with one
+        const V mo = wide::maj3(oc[b], o1, o2);  // box bits: >= 2 columns with a place
+        hb[b] = wide::mul24(wide::andn2(ob, tb, mo) & BOXC, 0x701C07u);  // boxes with one
+#if SDK_PLANE_LC
+        vp[b] = oc[b] & wide::mul24(wide::andn(wide::xor3(oc[b], o1, o2), mo) & BOXC, 7u);  // rule D
+#endif
     }
     const V O = wide::or3(oc[0], oc[1], oc[2]);
     const V hcol = wide::mul24(wide::andn2(O, wide::or3(tc[0], tc[1], tc[2]), wide::maj3(oc[0], oc[1], oc[2])) & 0x1FFu,
@@ -168,6 +175,26 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
         }
         eliminate(w, x2);
     }
+#if SDK_PLANE_LC
+    {
+        // ---- D (plane::pass rule D): a box whose places lie in one column
+        // takes the digit out of that column in the other bands; likewise
+        // for a row
+        const V vpa = wide::or3(vp[0], vp[1], vp[2]);
+        V lc = V(0u);
+#pragma unroll
+        for (int b = 0; b < 3; ++b) {
+#if SDK_PLANE_LC >= 2
+            const V e = wide::mul24(wide::andn(vpa, vp[b]), 0x100401u) | wide::point_rows(w[b]);
+#else
+            const V e = wide::mul24(wide::andn(vpa, vp[b]), 0x100401u);
+#endif
+            lc = lc | (w[b] & e);
+            w[b] = wide::andn(w[b], e);
+        }
+        newh = newh | wide::row_or(lc);
+    }
+#endif
     const M solved = wide::eq(all, V(ROWS));
     const M open = wide::ne(any_nd | newh, V(0u));
     return wide::pick(dead, V((uint32_t)DEAD), wide::pick(solved, V((uint32_t)SOLVED),

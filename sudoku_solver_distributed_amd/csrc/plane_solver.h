@@ -20,8 +20,13 @@
 //      box (a clash with an older determined cell empties that cell: dead);
 //   C. hidden singles: a digit with exactly one place in a unit goes there;
 //      a digit with no place in a unit kills the node; two digits forced into
-//      one cell kill it.
-// Rules B and C are sound only when the givens do not repeat a digit in a
+//      one cell kill it;
+//   D. locked candidates, pointing (SDK_PLANE_LC): a box whose places for a
+//      digit lie in one column takes the digit out of that column's cells in
+//      the other two bands (1: this only); one whose places lie in one row,
+//      out of that row's cells in the other two boxes (2: both).  Fewer
+//      passes and branch nodes for ~250 / ~500 VALU per pass.
+// Rules B, C and D are sound only when the givens do not repeat a digit in a
 // unit (the walk never tests givens, gen.py:8-28): such boards are reported
 // as `bad` by load() and left to the wave-per-board kernel, which handles
 // them.  Two determined cells sharing a digit in one unit are not flagged
@@ -56,6 +61,11 @@
 #endif
 #ifndef SDK_PLANE_PIN_ACC
 #define SDK_PLANE_PIN_ACC 1
+#endif
+// pass() rule D (locked candidates, pointing): 0 off, 1 box -> column,
+// 2 box -> column and box -> row (measured slower: DESIGN.md §4)
+#ifndef SDK_PLANE_LC
+#define SDK_PLANE_LC 1
 #endif
 
 namespace plane {
@@ -133,6 +143,19 @@ PS_FN uint32_t bop3_nor(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xE
 // 9-bit set (low 24 bits of c may hold no other bit) times k: one v_mul_u32_u24
 PS_FN uint32_t mul24(uint32_t c, uint32_t k) { return (c & 0xFFFFFFu) * k; }
 
+// rule D, box -> row, on one band word y of a digit's plane: the cells to
+// clear because a box of the band holds all its places in one row -- that
+// row outside the box.  (Two boxes pointing into two rows: each one's cells
+// in the other's row hold no place already.)  19 VALU.
+PS_FN uint32_t point_rows(uint32_t y)
+{
+    const uint32_t r3 = or3(y, y >> 1, y >> 2) & 0x4912449u;  // row k of box j has a place: bit 10k + 3j
+    const uint32_t a1 = r3 >> 10, a2 = r3 >> 20;
+    const uint32_t hbox = andn(xor3(r3, a1, a2), maj3(r3, a1, a2)) & BOXC;  // boxes with places in one row
+    const uint32_t rn = ((r3 & mul24(hbox, 0x100401u)) + ROWS) & GUARDS;   // the rows of those segments
+    return andn(rn - (rn >> 9), mul24(hbox, 0x701C07u));
+}
+
 PS_FN uint32_t spread_rows(uint32_t c) { return c | (c << 10) | (c << 20); }  // 9-bit column set -> 3 rows
 PS_FN uint32_t guard_rows(uint32_t g) { return g - (g >> 9); }               // guard flags -> whole rows
 PS_FN uint32_t row_nonzero(uint32_t y) { return (y + ROWS) & GUARDS; }        // guard set iff row != 0
@@ -153,6 +176,9 @@ PS_FN int pass(Board &B, uint32_t und[3])
 {
     uint32_t single[3], nd[3];
     uint32_t dead = 0;
+#if SDK_PLANE_LC
+    uint32_t lc = 0;  // rule D removed a place
+#endif
     // ---- A: determined cells.  o: >= 1 candidate, t: >= 2 candidates
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
@@ -203,6 +229,9 @@ PS_FN int pass(Board &B, uint32_t und[3])
         }
         // ---- C: hidden singles of d; units with no place left for d
         uint32_t o[3], t[3], gr[3], hb[3];
+#if SDK_PLANE_LC
+        uint32_t vp[3];  // rule D: per band, the column of each box whose places lie in one column
+#endif
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
             const uint32_t y = B.P[d][b];
@@ -218,8 +247,13 @@ PS_FN int pass(Board &B, uint32_t und[3])
             const uint32_t ob = or3(o[b], o1, o2);     // box bits 0/3/6: >= 1 place
             boxall &= ob;
             const uint32_t tb = or3(t[b], t[b] >> 1, t[b] >> 2);
-            const uint32_t q = andn2(ob, tb, maj3(o[b], o1, o2)) & BOXC;  // boxes with exactly one
+            const uint32_t mo = maj3(o[b], o1, o2);     // box bits: >= 2 columns with a place
+            const uint32_t q = andn2(ob, tb, mo) & BOXC;  // boxes with exactly one
             hb[b] = mul24(q, 0x701C07u);
+#if SDK_PLANE_LC
+            const uint32_t vb = andn(xor3(o[b], o1, o2), mo) & BOXC;  // boxes with exactly one column
+            vp[b] = o[b] & mul24(vb, 7u);
+#endif
         }
         const uint32_t O = or3(o[0], o[1], o[2]);
         colall &= O;
@@ -229,6 +263,25 @@ PS_FN int pass(Board &B, uint32_t und[3])
         // box.  Later digits drop these cells at their turn (above), earlier
         // ones after the loop.  A cell forced for two digits loses the later
         // one, whose unit then has no place for it: dead, as it must be.
+#if SDK_PLANE_LC
+        // ---- D: locked candidates (pointing): a box whose places for d lie
+        // in one column holds d's place of that column, so the column's
+        // cells in the other two bands lose d; likewise for a row
+        // (point_rows).  The singles of d see it next pass.
+        {
+            const uint32_t vpa = or3(vp[0], vp[1], vp[2]);
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+#if SDK_PLANE_LC >= 2
+                const uint32_t e = mul24(andn(vpa, vp[b]), 0x100401u) | point_rows(B.P[d][b]);
+#else
+                const uint32_t e = mul24(andn(vpa, vp[b]), 0x100401u);
+#endif
+                lc = or_and(lc, B.P[d][b], e);
+                B.P[d][b] = andn(B.P[d][b], e);
+            }
+        }
+#endif
 #pragma unroll
         for (int b = 0; b < 3; ++b)
             hall[b] = or_and(hall[b], B.P[d][b], bop3_nor(gr[b], hb[b], hcol));
@@ -240,6 +293,9 @@ PS_FN int pass(Board &B, uint32_t und[3])
         PS_PIN(rowall);
         PS_PIN(colall);
         PS_PIN(boxall);
+#if SDK_PLANE_LC
+        PS_PIN(lc);
+#endif
 #pragma unroll
         for (int b = 0; b < 3; ++b) PS_PIN(hall[b]);
 #endif
@@ -261,6 +317,9 @@ PS_FN int pass(Board &B, uint32_t und[3])
     if (dead) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = or3(hall[0] & und[0], hall[1] & und[1], hall[2] & und[2]) != 0;
+#if SDK_PLANE_LC
+    if (lc) return OPEN;
+#endif
     return (any_nd || newh) ? OPEN : STUCK;
 }
 

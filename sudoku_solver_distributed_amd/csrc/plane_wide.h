@@ -13,7 +13,8 @@
 // lines (plane_kernel.h PlaneStack), same branch rule -- so nothing is redone.
 //
 // Propagation is the same rule set as plane::pass (A naked singles, B peer
-// elimination, C hidden singles, dead units), with C's hidden singles applied
+// elimination, C hidden singles, dead units, D box -> column locked
+// candidates), with C's hidden singles applied
 // Jacobi-style (all digits at once; a cell forced for two digits is dead)
 // instead of Gauss-Seidel, and B run a second time for the cells forced this
 // pass.  Both passes are sound and reach the same fixpoints (up to when a
@@ -60,6 +61,8 @@ WD_FN M mor(M a, M b) { return a || b; }
 WD_FN V pick(M m, V a, V b) { return m ? a : b; }
 WD_FN V or3(V a, V b, V c) { return plane::or3(a, b, c); }
 WD_FN V maj3(V a, V b, V c) { return plane::maj3(a, b, c); }
+WD_FN V xor3(V a, V b, V c) { return plane::xor3(a, b, c); }
+WD_FN V point_rows(V y) { return plane::point_rows(y); }
 WD_FN V andn(V a, V b) { return plane::andn(a, b); }
 WD_FN V andn2(V a, V b, V c) { return plane::andn2(a, b, c); }
 WD_FN V sel(V m, V a, V b) { return plane::sel(m, a, b); }
@@ -150,11 +153,18 @@ WD_FN V pick(M m, const V &a, const V &b)
     }
 WD_F3(or3)
 WD_F3(maj3)
+WD_F3(xor3)
 WD_F3(andn2)
 WD_F3(sel)
 WD_F3(bop3_nor)
 #undef WD_F3
 WD_FN V andn(const V &a, const V &b) { return a & ~b; }
+WD_FN V point_rows(const V &y)
+{
+    V r;
+    for (int i = 0; i < 64; ++i) r.x[i] = plane::point_rows(y.x[i]);
+    return r;
+}
 WD_FN V mul24(const V &c, uint32_t k)
 {
     V r;
@@ -273,7 +283,8 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
     const V ob = or3(oc, o1, o2);
     dead = mor(dead, mand(L.valid, ne(ob & BOXC, V(BOXC))));  // a box with no place
     const V tb = or3(tc, tc >> 1, tc >> 2);
-    const V hb = mul24(andn2(ob, tb, maj3(oc, o1, o2)) & BOXC, 0x701C07u);  // boxes with one
+    const V mo = maj3(oc, o1, o2);  // box bits: >= 2 columns with a place
+    const V hb = mul24(andn2(ob, tb, mo) & BOXC, 0x701C07u);  // boxes with one
     const V oA = bperm(oc, L.src1), oB = bperm(oc, L.src2);
     const V tA = bperm(tc, L.src1), tB = bperm(tc, L.src2);
     const V O = or3(oc, oA, oB);
@@ -304,11 +315,28 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
         w = sel(or3(rn2 - (rn2 >> 9), cp2, mul24(g2 & BOXC, 0x701C07u)), x2, w);
     }
 #endif
+    bool lc = false;
+#if SDK_PLANE_LC
+    {
+        // ---- D (plane::pass rule D): a box whose places lie in one column
+        // takes d out of that column in the other bands (columns from this
+        // pass's y: a superset of the places now, so still sound); likewise
+        // for a row.
+        const V vp = oc & mul24(andn(xor3(oc, o1, o2), mo) & BOXC, 7u);
+#if SDK_PLANE_LC >= 2
+        const V e = mul24(andn(or3(vp, bperm(vp, L.src1), bperm(vp, L.src2)), vp), 0x100401u) | point_rows(w);
+#else
+        const V e = mul24(andn(or3(vp, bperm(vp, L.src1), bperm(vp, L.src2)), vp), 0x100401u);
+#endif
+        lc = ballot(ne(w & e, V(0u))) != 0;
+        w = andn(w, e);
+    }
+#endif
 
     if (ballot(dead)) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = ballot(ne(H & und, V(0u))) != 0;
-    return (any_nd || newh) ? OPEN : STUCK;
+    return (any_nd || newh || lc) ? OPEN : STUCK;
 }
 
 // fix the cell (band, pos) to digit bit dbit

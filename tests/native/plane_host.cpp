@@ -133,7 +133,7 @@ static uint32_t rnz(uint32_t y) { return (y + ROWS) & GUARDS; }
 static uint32_t fold(uint32_t y) { return (y | (y >> 10) | (y >> 20)) & 0x1FFu; }
 static int pass(Board &B, uint32_t und[3])
 {
-    uint32_t single[3], nd[3], dead = 0;
+    uint32_t single[3], nd[3], dead = 0, lc = 0;
     for (int b = 0; b < 3; ++b) {
         uint32_t o = 0, t = 0;
         for (int d = 0; d < 9; ++d) {
@@ -183,7 +183,39 @@ static int pass(Board &B, uint32_t und[3])
         const uint32_t T = t[0] | t[1] | t[2] | (o[0] & o[1]) | (o[2] & (o[0] | o[1]));
         colall &= O;
         const uint32_t hcol = spread(O & ~T);
-        for (int b = 0; b < 3; ++b) hall[b] |= hb[b] | (B.P[d][b] & hcol);
+#if SDK_PLANE_LC
+        // rule D: a box whose places lie in one column takes d out of that
+        // column in the other bands; one whose places lie in one row, out of
+        // that row in the other boxes
+        uint32_t vcol[3] = {0u, 0u, 0u};
+        for (int b = 0; b < 3; ++b)
+            for (int j = 0; j < 3; ++j) {
+                const uint32_t c = (o[b] >> (3 * j)) & 7u;
+                if (c && !(c & (c - 1))) vcol[b] |= c << (3 * j);
+            }
+        for (int b = 0; b < 3; ++b) {
+            uint32_t cols = 0;
+            for (int e = 0; e < 3; ++e)
+                if (e != b) cols |= vcol[e];
+            uint32_t m = spread(cols & ~vcol[b]);
+#if SDK_PLANE_LC >= 2
+            // a box whose places lie in one row: that row outside the boxes
+            // pointing into it (two boxes into one row: both kept)
+            uint32_t into[3] = {0u, 0u, 0u};
+            for (int j = 0; j < 3; ++j) {
+                int rows = 0;
+                for (int k = 0; k < 3; ++k)
+                    if ((B.P[d][b] >> (10 * k + 3 * j)) & 7u) rows |= 1 << k;
+                if (rows && !(rows & (rows - 1))) into[__builtin_ctz(rows)] |= 7u << (3 * j);
+            }
+            for (int k = 0; k < 3; ++k)
+                if (into[k]) m |= (0x1FFu & ~into[k]) << (10 * k);
+#endif
+            lc |= B.P[d][b] & m;
+            B.P[d][b] &= ~m;
+        }
+#endif
+        for (int b = 0; b < 3; ++b) hall[b] |= (hb[b] | hcol) & B.P[d][b];  // (after rule D)
     }
     for (int b = 0; b < 3; ++b) {
         uint32_t later = B.P[8][b];
@@ -196,7 +228,7 @@ static int pass(Board &B, uint32_t und[3])
     if (dead) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = ((hall[0] & und[0]) | (hall[1] & und[1]) | (hall[2] & und[2])) != 0;
-    return (any_nd || newh) ? OPEN : STUCK;
+    return (any_nd || newh || lc) ? OPEN : STUCK;
 }
 }  // namespace v1
 
