@@ -13,6 +13,9 @@
 #define WPE 4
 #endif
 #define ITER 256
+#ifndef VPP
+#define VPP 1463  // VALU per pass (profiles/isa_plane_pass.json)
+#endif
 
 __global__ __launch_bounds__(256, WPE) void pass_loop(const uint32_t *boards, uint32_t *sink, int nboards)
 {
@@ -62,8 +65,8 @@ int main(int argc, char **argv)
     hipEventElapsedTime(&ms, e0, e1);
     const double passes = (double)blocks * 256 * ITER * reps;
     printf("{\"cus\": %d, \"max_blocks_per_cu\": %d, \"waves_per_simd\": %d, \"ms\": %.3f, \"passes_per_s\": %.4g, "
-           "\"valu_frac_at_1495_per_pass\": %.3f}\n",
-           cus, bpc, blocks / cus, ms, passes / (ms * 1e-3), passes / (ms * 1e-3) * 1495 / 78.6432e12);
+           "\"valu_frac_at_%d_per_pass\": %.3f}\n",
+           cus, bpc, blocks / cus, ms, passes / (ms * 1e-3), VPP, passes / (ms * 1e-3) * VPP / 78.6432e12);
     }
     return 0;
 }

@@ -115,7 +115,7 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
 
     // ---- C: places of this lane's digit per row / box of each band, per column over the bands
     V oc[3], tc[3], gr[3], hb[3];
-#if SDK_PLANE_LC
+#if SDK_WIDE_LC
     V vp[3];
 #endif
     V rowall = V(GUARDS), boxall = V(BOXC);
@@ -136,7 +136,7 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
         const V tb = wide::or3(tc[b], tc[b] >> 1, tc[b] >> 2);
         const V mo = wide::maj3(oc[b], o1, o2);  // box bits: >= 2 columns with a place
         hb[b] = wide::mul24(wide::andn2(ob, tb, mo) & BOXC, 0x701C07u);  // boxes with one
-#if SDK_PLANE_LC
+#if SDK_WIDE_LC
         vp[b] = oc[b] & wide::mul24(wide::andn(wide::xor3(oc[b], o1, o2), mo) & BOXC, 7u);  // rule D
 #endif
     }
@@ -175,19 +175,31 @@ WD_FN V pass(V (&w)[3], V (&det)[3], V (&und)[3], const Lanes &L)
         }
         eliminate(w, x2);
     }
-#if SDK_PLANE_LC
+#if SDK_WIDE_LC
     {
         // ---- D (plane::pass rule D): a box whose places lie in one column
         // takes the digit out of that column in the other bands; likewise
         // for a row
         const V vpa = wide::or3(vp[0], vp[1], vp[2]);
+        const V one_band = wide::andn(wide::xor3(oc[0], oc[1], oc[2]), wide::maj3(oc[0], oc[1], oc[2])) & 0x1FFu;
+        (void)vpa;
+        (void)one_band;
         V lc = V(0u);
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-#if SDK_PLANE_LC >= 2
-            const V e = wide::mul24(wide::andn(vpa, vp[b]), 0x100401u) | wide::point_rows(w[b]);
-#else
-            const V e = wide::mul24(wide::andn(vpa, vp[b]), 0x100401u);
+            V ec = V(0u);
+#if SDK_WIDE_LC & 1
+            ec = wide::andn(vpa, vp[b]);
+#endif
+#if SDK_WIDE_LC & 4
+            {
+                const V cc = oc[b] & one_band;
+                ec = ec | wide::andn(wide::mul24(wide::or3(cc, cc >> 1, cc >> 2) & BOXC, 7u), cc);
+            }
+#endif
+            V e = wide::mul24(ec, 0x100401u);
+#if SDK_WIDE_LC & 2
+            e = e | wide::point_rows(w[b]);
 #endif
             lc = lc | (w[b] & e);
             w[b] = wide::andn(w[b], e);

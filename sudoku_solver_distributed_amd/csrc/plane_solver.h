@@ -21,11 +21,12 @@
 //   C. hidden singles: a digit with exactly one place in a unit goes there;
 //      a digit with no place in a unit kills the node; two digits forced into
 //      one cell kill it;
-//   D. locked candidates, pointing (SDK_PLANE_LC): a box whose places for a
+//   D. locked candidates (SDK_PLANE_LC flags): a box whose places for a
 //      digit lie in one column takes the digit out of that column's cells in
-//      the other two bands (1: this only); one whose places lie in one row,
-//      out of that row's cells in the other two boxes (2: both).  Fewer
-//      passes and branch nodes for ~250 / ~500 VALU per pass.
+//      the other two bands (1, the default); one whose places lie in one
+//      row, out of that row's cells in the other two boxes (2); a column
+//      whose places lie in one band, out of the rest of its box (4).  Fewer
+//      passes and branch nodes for ~250 VALU per pass.
 // Rules B, C and D are sound only when the givens do not repeat a digit in a
 // unit (the walk never tests givens, gen.py:8-28): such boards are reported
 // as `bad` by load() and left to the wave-per-board kernel, which handles
@@ -62,10 +63,15 @@
 #ifndef SDK_PLANE_PIN_ACC
 #define SDK_PLANE_PIN_ACC 1
 #endif
-// pass() rule D (locked candidates, pointing): 0 off, 1 box -> column,
-// 2 box -> column and box -> row (measured slower: DESIGN.md §4)
+// pass() rule D (locked candidates), flags: 1 box -> column, 2 box -> row,
+// 4 column -> box; 0 off (only 1 pays: DESIGN.md §4)
 #ifndef SDK_PLANE_LC
 #define SDK_PLANE_LC 1
+#endif
+// the same flags for the wave-wide and four-board tail solvers (plane_wide.h,
+// plane_quad.h), whose passes are latency- rather than issue-bound
+#ifndef SDK_WIDE_LC
+#define SDK_WIDE_LC SDK_PLANE_LC
 #endif
 
 namespace plane {
@@ -257,7 +263,8 @@ PS_FN int pass(Board &B, uint32_t und[3])
         }
         const uint32_t O = or3(o[0], o[1], o[2]);
         colall &= O;
-        const uint32_t hc = andn2(O, or3(t[0], t[1], t[2]), maj3(o[0], o[1], o[2])) & 0x1FFu;
+        const uint32_t mo3 = maj3(o[0], o[1], o[2]);  // columns with places in >= 2 bands
+        const uint32_t hc = andn2(O, or3(t[0], t[1], t[2]), mo3) & 0x1FFu;
         const uint32_t hcol = mul24(hc, 0x100401u);
         // d's hidden singles: the cells of y alone in their row, column or
         // box.  Later digits drop these cells at their turn (above), earlier
@@ -270,12 +277,26 @@ PS_FN int pass(Board &B, uint32_t und[3])
         // (point_rows).  The singles of d see it next pass.
         {
             const uint32_t vpa = or3(vp[0], vp[1], vp[2]);
+            const uint32_t one_band = andn(xor3(o[0], o[1], o[2]), mo3) & 0x1FFu;  // columns with places in one band
+            (void)vpa;
+            (void)one_band;
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
-#if SDK_PLANE_LC >= 2
-                const uint32_t e = mul24(andn(vpa, vp[b]), 0x100401u) | point_rows(B.P[d][b]);
-#else
-                const uint32_t e = mul24(andn(vpa, vp[b]), 0x100401u);
+                uint32_t ec = 0;  // columns of the band to clear
+#if SDK_PLANE_LC & 1
+                ec = andn(vpa, vp[b]);
+#endif
+#if SDK_PLANE_LC & 4
+                {
+                    // column -> box: a column whose places lie in this band
+                    // holds the box's place: the box's other columns lose d
+                    const uint32_t cc = o[b] & one_band;
+                    ec |= andn(mul24(or3(cc, cc >> 1, cc >> 2) & BOXC, 7u), cc);
+                }
+#endif
+                uint32_t e = mul24(ec, 0x100401u);
+#if SDK_PLANE_LC & 2
+                e |= point_rows(B.P[d][b]);
 #endif
                 lc = or_and(lc, B.P[d][b], e);
                 B.P[d][b] = andn(B.P[d][b], e);

@@ -316,17 +316,26 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
     }
 #endif
     bool lc = false;
-#if SDK_PLANE_LC
+#if SDK_WIDE_LC
     {
         // ---- D (plane::pass rule D): a box whose places lie in one column
         // takes d out of that column in the other bands (columns from this
         // pass's y: a superset of the places now, so still sound); likewise
         // for a row.
         const V vp = oc & mul24(andn(xor3(oc, o1, o2), mo) & BOXC, 7u);
-#if SDK_PLANE_LC >= 2
-        const V e = mul24(andn(or3(vp, bperm(vp, L.src1), bperm(vp, L.src2)), vp), 0x100401u) | point_rows(w);
-#else
-        const V e = mul24(andn(or3(vp, bperm(vp, L.src1), bperm(vp, L.src2)), vp), 0x100401u);
+        V ec = V(0u);
+#if SDK_WIDE_LC & 1
+        ec = andn(or3(vp, bperm(vp, L.src1), bperm(vp, L.src2)), vp);
+#endif
+#if SDK_WIDE_LC & 4
+        {
+            const V cc = oc & (andn(xor3(oc, oA, oB), maj3(oc, oA, oB)) & 0x1FFu);  // columns only in this band
+            ec = ec | andn(mul24(or3(cc, cc >> 1, cc >> 2) & BOXC, 7u), cc);
+        }
+#endif
+        V e = mul24(ec, 0x100401u);
+#if SDK_WIDE_LC & 2
+        e = e | point_rows(w);
 #endif
         lc = ballot(ne(w & e, V(0u))) != 0;
         w = andn(w, e);

@@ -197,8 +197,25 @@ static int pass(Board &B, uint32_t und[3])
             uint32_t cols = 0;
             for (int e = 0; e < 3; ++e)
                 if (e != b) cols |= vcol[e];
-            uint32_t m = spread(cols & ~vcol[b]);
-#if SDK_PLANE_LC >= 2
+            uint32_t ec = 0;
+#if SDK_PLANE_LC & 1
+            ec = cols & ~vcol[b];
+#endif
+#if SDK_PLANE_LC & 4
+            // a column whose places lie in this band only: the other columns
+            // of its box (all of the band's such columns kept)
+            uint32_t claimed = 0;
+            for (int c = 0; c < 9; ++c) {
+                int bands = 0;
+                for (int e = 0; e < 3; ++e)
+                    if ((o[e] >> c) & 1u) bands |= 1 << e;
+                if (bands == (1 << b)) claimed |= 1u << c;
+            }
+            for (int j = 0; j < 3; ++j)
+                if ((claimed >> (3 * j)) & 7u) ec |= (7u << (3 * j)) & ~claimed;
+#endif
+            uint32_t m = spread(ec);
+#if SDK_PLANE_LC & 2
             // a box whose places lie in one row: that row outside the boxes
             // pointing into it (two boxes into one row: both kept)
             uint32_t into[3] = {0u, 0u, 0u};

@@ -14,12 +14,15 @@ from conftest import b81, load_golden
 from oracle import oracle as O
 
 NATIVE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "native")
+# extra compiler flags for the host builds, e.g. SDK_HOST_CFLAGS="-DSDK_PLANE_LC=7"
+# to check a rule-D variant against its restatement
+HOST_FLAGS = os.environ.get("SDK_HOST_CFLAGS", "").split()
 
 
 @pytest.fixture(scope="module")
 def host(tmp_path_factory):
     out = os.path.join(str(tmp_path_factory.mktemp("plane")), "libplane_host.so")
-    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-o", out,
+    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", *HOST_FLAGS, "-o", out,
                            os.path.join(NATIVE, "plane_host.cpp")])
     lib = ctypes.CDLL(out)
     lib.plane_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
@@ -178,7 +181,7 @@ def test_pass_matches_previous_formulation(host):
 @pytest.fixture(scope="module")
 def wide(tmp_path_factory):
     out = os.path.join(str(tmp_path_factory.mktemp("wide")), "libwide_host.so")
-    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-o", out,
+    subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", *HOST_FLAGS, "-o", out,
                            os.path.join(NATIVE, "wide_host.cpp")])
     lib = ctypes.CDLL(out)
     lib.wide_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
