@@ -349,3 +349,31 @@ def test_split_count_vs_oracle(wide, order, mrv):
         assert total > 100  # the count was really dealt out
     finally:
         wide.wide_set_mrv_after(0)
+
+
+@pytest.mark.parametrize("flags", [0, 3, 5, 7])
+def test_rule_d_variants_match_their_restatement(tmp_path, flags):
+    """Every SDK_PLANE_LC rule-D variant (0 none, 1 box -> column -- the
+    default, covered above --, 2 box -> row, 4 column -> box) keeps the
+    pass equal to its plain-loop restatement (plane_host.cpp v1::pass) after
+    every pass, and the wave-wide and four-board passes reach its fixpoints
+    (wide_host.cpp), so a build with other flags stays exact."""
+    define = "-DSDK_PLANE_LC=%d" % flags
+    libs = {}
+    for name in ("plane_host", "wide_host"):
+        out = str(tmp_path / ("lib%s_%d.so" % (name, flags)))
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", define, "-o", out,
+                               os.path.join(NATIVE, name + ".cpp")])
+        libs[name] = ctypes.CDLL(out)
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    boards = np.ascontiguousarray(np.concatenate([hard17_batch(150, seed=21).numpy(),
+                                                  hard_search_batch(150, seed=22).numpy()]))
+    chk = libs["plane_host"].plane_check_pass
+    chk.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64]
+    chk.restype = ctypes.c_int64
+    assert chk(boards.ctypes.data, len(boards), 50_000, 5) == 0
+    for fn in ("wide_check_fixpoint", "quad_check_fixpoint"):
+        f = getattr(libs["wide_host"], fn)
+        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
+        f.restype = ctypes.c_int64
+        assert f(boards[:100].ctypes.data, 100, 5, 3) == 0, fn
