@@ -68,6 +68,11 @@
 #ifndef SDK_PLANE_MRV
 #define SDK_PLANE_MRV 64
 #endif
+// every how many lane-loop iterations the pass also applies rule D's box ->
+// row form (plane_solver.h; 0 never)
+#ifndef SDK_PLANE_ROWS_PERIOD
+#define SDK_PLANE_ROWS_PERIOD 0
+#endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
 #endif
@@ -1485,6 +1490,9 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         }
     }
 
+#if SDK_PLANE_ROWS_PERIOD
+    int rows_ctr = 0;
+#endif
     for (;;) {
 #if SDK_PLANE_STAMPS
         const uint64_t st_ta = __builtin_amdgcn_s_memtime();
@@ -1494,6 +1502,9 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             if (!st_t1) st_t1 = __builtin_amdgcn_s_memrealtime();
             st_after++;
         }
+#endif
+#if SDK_PLANE_ROWS_PERIOD
+        rows_ctr = __builtin_amdgcn_readfirstlane(rows_ctr + 1 == SDK_PLANE_ROWS_PERIOD ? 0 : rows_ctr + 1);  // every lane is here
 #endif
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
         if (__builtin_popcountll(~active) >= refill || active == 0) {
@@ -1801,7 +1812,13 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         st_piters++;
 #endif
         uint32_t und[3];
+#if SDK_PLANE_ROWS_PERIOD
+        // rule D's box -> row form on every SDK_PLANE_ROWS_PERIOD-th
+        // iteration of the wave (a wave-uniform choice: one pass body runs)
+        const int r = plane::pass(B, und, rows_ctr == 0);
+#else
         const int r = plane::pass(B, und);
+#endif
         if (r == plane::STUCK && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
             state = PL_CANCELLED;  // ordered mode: a lower board is solved
             continue;

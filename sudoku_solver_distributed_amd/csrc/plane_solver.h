@@ -64,7 +64,9 @@
 #define SDK_PLANE_PIN_ACC 1
 #endif
 // pass() rule D (locked candidates), flags: 1 box -> column, 2 box -> row,
-// 4 column -> box; 0 off (only 1 pays: DESIGN.md §4)
+// 4 column -> box; 0 off (only 1 pays on every pass: DESIGN.md §4).  The
+// box -> row form can also run on every SDK_PLANE_ROWS_PERIOD-th pass of the
+// plane kernel's lane loop only (pass()'s point_rows_on; plane_kernel.h)
 #ifndef SDK_PLANE_LC
 #define SDK_PLANE_LC 1
 #endif
@@ -178,7 +180,9 @@ PS_FN void pin_board(Board &B);
 // with literal constants, three-input logic as v_bitop3_b32 on VGPRs, right
 // shifts only, and one v_mul_u32_u24 per spread of a 9-bit set over three
 // rows.  ~1380 issue slots per pass (profiles/isa_plane_pass.json).
-PS_FN int pass(Board &B, uint32_t und[3])
+// point_rows_on: rule D's box -> row form this pass (wave-uniform on the
+// GPU: one scalar branch after the digit loop)
+PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2) != 0)
 {
     uint32_t single[3], nd[3];
     uint32_t dead = 0;
@@ -294,10 +298,7 @@ PS_FN int pass(Board &B, uint32_t und[3])
                     ec |= andn(mul24(or3(cc, cc >> 1, cc >> 2) & BOXC, 7u), cc);
                 }
 #endif
-                uint32_t e = mul24(ec, 0x100401u);
-#if SDK_PLANE_LC & 2
-                e |= point_rows(B.P[d][b]);
-#endif
+                const uint32_t e = mul24(ec, 0x100401u);
                 lc = or_and(lc, B.P[d][b], e);
                 B.P[d][b] = andn(B.P[d][b], e);
             }
@@ -334,6 +335,22 @@ PS_FN int pass(Board &B, uint32_t und[3])
             if (e) later |= B.P[e][b];
         }
     }
+#if SDK_PLANE_LC
+    if (point_rows_on) {
+        // rule D's box -> row form, after the digit loop (its registers are
+        // free again): every plane word once
+#pragma unroll
+        for (int d = 0; d < 9; ++d)
+#pragma unroll
+            for (int b = 0; b < 3; ++b) {
+                const uint32_t e = point_rows(B.P[d][b]);
+                lc = or_and(lc, B.P[d][b], e);
+                B.P[d][b] = andn(B.P[d][b], e);
+                PS_PIN(B.P[d][b]);
+                PS_PIN(lc);
+            }
+    }
+#endif
     dead |= or3(rowall ^ GUARDS, colall ^ 0x1FFu, (boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;
     if (all_single) return SOLVED;

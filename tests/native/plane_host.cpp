@@ -215,19 +215,9 @@ static int pass(Board &B, uint32_t und[3])
                 if ((claimed >> (3 * j)) & 7u) ec |= (7u << (3 * j)) & ~claimed;
 #endif
             uint32_t m = spread(ec);
-#if SDK_PLANE_LC & 2
-            // a box whose places lie in one row: that row outside the boxes
-            // pointing into it (two boxes into one row: both kept)
-            uint32_t into[3] = {0u, 0u, 0u};
-            for (int j = 0; j < 3; ++j) {
-                int rows = 0;
-                for (int k = 0; k < 3; ++k)
-                    if ((B.P[d][b] >> (10 * k + 3 * j)) & 7u) rows |= 1 << k;
-                if (rows && !(rows & (rows - 1))) into[__builtin_ctz(rows)] |= 7u << (3 * j);
-            }
-            for (int k = 0; k < 3; ++k)
-                if (into[k]) m |= (0x1FFu & ~into[k]) << (10 * k);
-#endif
+            lc |= B.P[d][b] & m;
+            B.P[d][b] &= ~m;
+            m = 0;
             lc |= B.P[d][b] & m;
             B.P[d][b] &= ~m;
         }
@@ -241,6 +231,25 @@ static int pass(Board &B, uint32_t und[3])
             if (e) later |= B.P[e][b];
         }
     }
+#if SDK_PLANE_LC & 2
+    // rule D, box -> row, after the digit loop: a box whose places lie in
+    // one row takes the digit out of that row outside the boxes pointing
+    // into it (two boxes into one row: both kept)
+    for (int d = 0; d < 9; ++d)
+        for (int b = 0; b < 3; ++b) {
+            uint32_t into[3] = {0u, 0u, 0u}, m = 0;
+            for (int j = 0; j < 3; ++j) {
+                int rows = 0;
+                for (int k = 0; k < 3; ++k)
+                    if ((B.P[d][b] >> (10 * k + 3 * j)) & 7u) rows |= 1 << k;
+                if (rows && !(rows & (rows - 1))) into[__builtin_ctz(rows)] |= 7u << (3 * j);
+            }
+            for (int k = 0; k < 3; ++k)
+                if (into[k]) m |= (0x1FFu & ~into[k]) << (10 * k);
+            lc |= B.P[d][b] & m;
+            B.P[d][b] &= ~m;
+        }
+#endif
     dead |= (rowall ^ GUARDS) | (colall ^ 0x1FFu) | ((boxall & BOXC) ^ BOXC);
     if (dead) return DEAD;
     if (all_single) return SOLVED;
