@@ -1186,6 +1186,10 @@ __device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane
         int r = busy ? (int)r0 : quad::OPEN;
         mst += busy ? 1u : 0u;
         int mode = plane::mst_mode(mst);
+        if (busy && r == quad::STUCK && plane::root_counts(mode, depth, mrv_after, und[0], und[1], und[2])) {
+            mode = plane::M_COUNT;  // a wide-open root: count at once (plane::search_step)
+            mst = plane::mst_set_mode(mst, plane::M_COUNT);
+        }
         int res = Q_SEARCHING;  // the row's answer (wide::W_*; W_OVERFLOW is -1)
         int reload = -1;       // a level whose planes replace the row's board
         bool scan = false;     // reload scans down for an untried digit

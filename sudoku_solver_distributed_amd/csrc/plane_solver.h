@@ -618,6 +618,22 @@ PS_FN uint32_t mst_set_mode(uint32_t mst, int mode) { return (mst & MST_PASSES) 
 
 enum { S_CONT = 0, S_SOLVED = 1, S_NONE = 2, S_DEEP = 3 };
 
+// A board whose propagated root still has at least SDK_PLANE_ROOT_OPEN
+// undetermined cells starts in M_COUNT at once (0: never; only when the
+// switch is on at all, mrv_after != 0).  Propagation that settles almost
+// nothing at the root (17 clues, 60+ open cells: a quarter of the corpus)
+// leaves the walk's fixed cell order nothing to lean on, and the
+// fewest-candidates count is cheaper there; boards the root propagation
+// opens up keep the walk's quick answers.
+#ifndef SDK_PLANE_ROOT_OPEN
+#define SDK_PLANE_ROOT_OPEN 58
+#endif
+PS_FN bool root_counts(int mode, uint32_t depth, uint32_t mrv_after, uint32_t u0, uint32_t u1, uint32_t u2)
+{
+    return SDK_PLANE_ROOT_OPEN && mrv_after && mode == M_WALK && depth == 0 &&
+           __builtin_popcount(u0) + __builtin_popcount(u1) + __builtin_popcount(u2) >= SDK_PLANE_ROOT_OPEN;
+}
+
 // One search step after a pass with result r (the lane solver's, and the
 // plane kernel's lane loop: both call this).  Stack: push(level, B, entry),
 // pop(level, B) -> entry (the level's planes into B, entry with them),
@@ -630,7 +646,11 @@ PS_FN int search_step(Board &B, const uint32_t (&und)[3], int r, uint32_t &depth
                       int node_order, uint32_t max_depth, uint32_t mrv_after, uint32_t &guesses)
 {
     mst++;
-    const int mode = mst_mode(mst);
+    int mode = mst_mode(mst);
+    if (r == STUCK && root_counts(mode, depth, mrv_after, und[0], und[1], und[2])) {
+        mode = M_COUNT;  // count from the root, branching right here
+        mst = mst_set_mode(mst, M_COUNT);
+    }
     const uint32_t sol_level = max_depth - 1;  // M_COUNT keeps its first completion here
     // every plane load of the step at one site (the end): the level whose
     // planes replace the board's -- the next untried digit's, the root, or

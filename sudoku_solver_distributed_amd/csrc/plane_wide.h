@@ -404,7 +404,12 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
         st.passes++;
         int r = pass(w, det, und, L);
         mst++;
-        const int mode = plane::mst_mode(mst);
+        int mode = plane::mst_mode(mst);
+        if (r == STUCK && plane::root_counts(mode, depth, mrv_after, rdl(und, 0), rdl(und, 16), rdl(und, 32))) {
+            mode = plane::M_COUNT;  // a wide-open root: count at once (plane::search_step)
+            mst = plane::mst_set_mode(mst, plane::M_COUNT);
+            hk.counting(true);
+        }
         if (mode == plane::M_WALK && mrv_after && r != SOLVED && (mst & plane::MST_PASSES) >= mrv_after) {
             if (depth) w = stk.restore(0, L);  // the propagated root
             det = V(0u);
