@@ -377,3 +377,30 @@ def test_rule_d_variants_match_their_restatement(tmp_path, flags):
         f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
         f.restype = ctypes.c_int64
         assert f(boards[:100].ctypes.data, 100, 5, 3) == 0, fn
+
+
+def test_open_root_rule_same_answers_fewer_passes(tmp_path):
+    """SDK_PLANE_ROOT_OPEN (plane_solver.h): a board whose propagated root
+    keeps >= 58 open cells counts its completions from the root at once.
+    Same answers and statuses as without the rule (the count's one
+    completion is the walk's answer), fewer passes on the 17-clue corpus."""
+    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
+    boards = np.ascontiguousarray(np.concatenate([hard17_batch(1500, seed=31).numpy(),
+                                                  hard_search_batch(300, seed=32).numpy()]))
+    res = {}
+    for t in (0, 58):
+        out = str(tmp_path / ("libplane_root%d.so" % t))
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", "-DSDK_PLANE_ROOT_OPEN=%d" % t,
+                               "-o", out, os.path.join(NATIVE, "plane_host.cpp")])
+        lib = ctypes.CDLL(out)
+        lib.plane_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        lib.plane_set_mrv_after.argtypes = [ctypes.c_uint32]
+        lib.plane_set_mrv_after(64)
+        stats = {}
+        sols, st = _solve(lib, boards, stats=stats)
+        hard = {}
+        _solve(lib, boards[:1500], stats=hard)
+        res[t] = (sols, st, hard["passes"])
+    assert np.array_equal(res[0][0], res[58][0]) and np.array_equal(res[0][1], res[58][1])
+    assert res[58][2] < 0.95 * res[0][2], (res[0][2], res[58][2])
