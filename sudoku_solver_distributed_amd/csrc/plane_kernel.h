@@ -45,7 +45,7 @@
 #define SDK_PLANE_REFILL 3
 #endif
 #ifndef SDK_PLANE_TAIL
-#define SDK_PLANE_TAIL 12
+#define SDK_PLANE_TAIL 6  // 12 until rule D and the open-root count shortened the heavy boards
 #endif
 // 3: continue through the XCD's tail pool on the four-board solver
 // (plane_quad.h), 2: the same on the wave-wide solver, 1: the wave-wide
