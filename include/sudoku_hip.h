@@ -172,11 +172,10 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream);
  * solve launch adds its board count to the workspace, each board's answer
  * (any status) counts once as finished, and a kernel that could not finish a
  * board it had taken sets an error word (SDK_ERR_* bits: 1 = a tail-pool
- * record it had claimed was never published, 2 = tail-pool waves waited
- * ~0.25 s on a count-mode board that never ended).  out (may be
+ * record it had claimed was never published).  out (may be
  * NULL): out[0] boards assigned, out[1] boards finished, out[2] error bits,
- * all since the last sdk_read_stats(reset) / report; out[3] times a
- * count-mode search dealt subtrees out to other waves (statistics).  Returns 0 when
+ * all since the last sdk_read_stats(reset) / report; out[3] reserved (0).
+ * Returns 0 when
  * assigned == finished and no error bit is set; -3 otherwise (text in
  * sdk_last_error(); the error word is then cleared and the counts re-synced,
  * so each fault is reported once); -1 HIP error; -2 bad arguments. */
@@ -205,9 +204,9 @@ int sdk_set_solve_kernel(int kernel);
  * defaults are the measured optimum).  refill: idle lanes
  * before a wave refills; tail: active lanes at or below which a drained wave
  * hands its last boards to the tail solver (0 off, at most 40); tail_mode: 1
- * the wave-wide solver continues each search, 2 the same through a per-XCD
- * pool that every exiting wave of the XCD drains, 3 that pool drained four
- * boards per wave (plane_quad.h), 0 the wave-per-board solver restarts it; chunk: most boards a wave claims from the queue at once (at
+ * the wave-wide solver continues each search on the wave itself, 2 the same
+ * through a per-XCD pool that every exiting wave of the XCD drains; chunk:
+ * most boards a wave claims from the queue at once (at
  * most 64: a claim is staged and converted in one go; 0 one claim per refill).  A
  * negative value keeps that knob; all four negative restore the defaults
  * ($SDK_PLANE_REFILL / _TAIL / _TAIL_MODE / _CHUNK).  Results never depend on

@@ -31,7 +31,7 @@ solver.stats(reset=True)
 solver.solve(boards, grid_waves=gw)
 torch.cuda.synchronize()
 v = solver.verify()
-print(f"split deals {v['splits']}, boards answered {v['finished']} of {v['assigned']}")
+print(f"boards answered {v['finished']} of {v['assigned']}")
 pd = ws[24 * 8:30 * 8].view(torch.int64).cpu().numpy()
 if pd[0] or pd[1]:
     print(f"tail pool: {pd[0]} claims, {pd[1]} failed claims, {pd[2]} flag polls; kcycles claiming {pd[3] / 1e3:.0f}, waiting {pd[4] / 1e3:.0f}, solving {pd[5] / 1e3:.0f}")

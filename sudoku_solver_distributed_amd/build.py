@@ -34,7 +34,6 @@ VARIANTS = {
     "waves5": (("SDK_PLANE_WAVES_PER_EU=5",), _SCHED),
     "waves6": (("SDK_PLANE_WAVES_PER_EU=6",), _SCHED),
     "nopinacc": (("SDK_PLANE_PIN_ACC=0",), _SCHED),
-    "tail_restart": (("SDK_PLANE_TAIL_MODE=0",), _SCHED),
     "sched-default": ((), "default"),
     "sched-minreg": ((), "iterative-minreg"),
     "sched-maxocc": ((), "iterative-maxocc"),

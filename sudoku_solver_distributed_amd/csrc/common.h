@@ -34,13 +34,11 @@ enum {
     WS_DEFERRED = 12,  // boards the plane kernel left to the packed kernel
     WS_ASSIGNED = 13,  // boards handed to the solve kernels (each launch adds its n): == WS_FINISHED once done
     WS_ERROR = 14,     // SDK_ERR_* bits, sticky until sdk_verify_workspace reports them
-    WS_SPLITS = 15,    // statistics: split-count deals in the tail pool (plane_kernel.h PoolHook)
+    WS_RESERVED = 15,  // always 0 (sdk_read_stats / sdk_verify_workspace out[3])
     WS_WORDS = 16
 };
 // WS_ERROR bits
 #define SDK_ERR_POOL_WAIT 1u  // a pool consumer gave up waiting on a claimed record: that board was not solved
-#define SDK_ERR_POOL_IDLE 2u  // waves waited ~0.25 s for a count-mode board to deal out work (a counting leak)
-#define SDK_ERR_QUAD_STALL 4u // the four-board tail solver ran ~4 M passes without finishing (a search bug)
 
 __device__ __forceinline__ uint32_t lowbit(uint32_t x) { return x & (0u - x); }
 
@@ -118,25 +116,18 @@ int sdk_plane_blocks_per_cu();
 // than this and the wave kernel finds them by scanning the statuses)
 #define PLANE_DEFER_CAP (1 << 20)
 // The drained waves' tail pool (plane_kernel.h, tail mode 2), after the
-// deferred list: per XCD, two 128-byte control lines (re-armed every call:
-// slots reserved, records published, slots taken and descriptors handed out
-// on one; count-mode boards being solved and waves waiting for work, which
-// the waiting waves poll, on the other), PLANE_POOL_CAP records of PLANE_POOL_REC dwords, one ready
-// flag (uint32) per record, then PLANE_POOL_DESCS split descriptors of
-// PLANE_POOL_DESC_WORDS dwords (a count-mode board whose subtrees are dealt
-// out over several waves).  A ready flag holds the launch generation
-// (WS_GEN) of the record it publishes, so flags need no clearing: one left
-// by an earlier launch (or set after its consumer gave up) never matches a
-// later launch's generation.
+// deferred list: per XCD, one 128-byte control line (slots reserved, records
+// published, slots taken; re-armed every call), PLANE_POOL_CAP records of
+// PLANE_POOL_REC dwords, then one ready flag (uint32) per record.  A ready
+// flag holds the launch generation (WS_GEN) of the record it publishes, so
+// flags need no clearing: one left by an earlier launch (or set after its
+// consumer gave up) never matches a later launch's generation.
 #define PLANE_POOL_XCDS 8
 #define PLANE_POOL_CAP 16384
 #define PLANE_POOL_REC 36
-#define PLANE_POOL_CTL 64  // two 128-byte lines: claims (words 0..3), waiting waves' polls (32..33)
-#define PLANE_POOL_ARM_WORDS 8  // words 0..3 and 32..35 of the control lines
-#define PLANE_POOL_DESCS 1024
-#define PLANE_POOL_DESC_WORDS 64
-#define PLANE_POOL_STRIDE \
-    (PLANE_POOL_CTL + PLANE_POOL_CAP * (PLANE_POOL_REC + 1) + PLANE_POOL_DESCS * PLANE_POOL_DESC_WORDS)  // dwords per XCD
+#define PLANE_POOL_CTL 32       // one 128-byte line
+#define PLANE_POOL_ARM_WORDS 4  // its words 0..3
+#define PLANE_POOL_STRIDE (PLANE_POOL_CTL + PLANE_POOL_CAP * (PLANE_POOL_REC + 1))  // dwords per XCD
 #define PLANE_POOL_BYTES ((size_t)PLANE_POOL_XCDS * PLANE_POOL_STRIDE * 4)
 
 #endif  // SDK_COMMON_H

@@ -35,9 +35,7 @@
 #define SDK_PLANE_KERNEL_H
 
 #include "plane_solver.h"
-#include "packed_solver.h"
 #include "plane_wide.h"
-#include "plane_quad.h"
 
 // defaults of the runtime knobs (plane_kernels.hip: $SDK_PLANE_REFILL,
 // $SDK_PLANE_TAIL, $SDK_PLANE_TAIL_MODE, $SDK_PLANE_CHUNK)
@@ -47,9 +45,8 @@
 #ifndef SDK_PLANE_TAIL
 #define SDK_PLANE_TAIL 6  // 12 until rule D and the open-root count shortened the heavy boards
 #endif
-// 3: continue through the XCD's tail pool on the four-board solver
-// (plane_quad.h), 2: the same on the wave-wide solver, 1: the wave-wide
-// solver on the wave's own boards only, 0: restart on the wave-per-board solver
+// 2: continue through the XCD's tail pool on the wave-wide solver, 1: the
+// wave-wide solver on the wave's own boards only
 #ifndef SDK_PLANE_TAIL_MODE
 #define SDK_PLANE_TAIL_MODE 2
 #endif
@@ -68,19 +65,8 @@
 #ifndef SDK_PLANE_MRV
 #define SDK_PLANE_MRV 64
 #endif
-// every how many lane-loop iterations the pass also applies rule D's box ->
-// row form (plane_solver.h; 0 never)
-#ifndef SDK_PLANE_ROWS_PERIOD
-#define SDK_PLANE_ROWS_PERIOD 0
-#endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
-#endif
-// 1: a claimed chunk is converted once, lane-parallel, into value bit-slice
-// records that refills hand out (plane_convert_chunk); 0: each refill stages
-// its boards and deposits them one at a time by ballots
-#ifndef SDK_PLANE_PRECONV
-#define SDK_PLANE_PRECONV 1
 #endif
 // diagnostic builds only (build.py --tag stamps -DSDK_PLANE_STAMPS=1): per
 // wave, s_memrealtime (100 MHz) at start, when the queue drained and at exit,
@@ -91,9 +77,6 @@
 #endif
 static_assert(plane::STACK_ENTRY == 27, "stack layout");
 typedef uint32_t sdk_v4u __attribute__((ext_vector_type(4)));
-// v_writelane_b32 (this clang has no builtin for it): the LLVM intrinsic,
-// so the compiler places the lane select in m0 and handles the hazards
-__device__ int llvm_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 
 // Per-lane DFS stack in the workspace: level L of lane g is one 128-byte
 // line at byte (g * PLANE_MAX_DEPTH + L) * 128, words 0..26 = the 27 planes
@@ -310,30 +293,6 @@ struct PlaneIOn {
     __device__ __forceinline__ int64_t seg_local(int64_t v) const { return v - start(batch(v)); }
 };
 
-// A drained wave's last boards (lanes `act`, board index p_lo / p_hi per
-// lane), each restarted on the whole wave by the wave-per-board solver.  Runs
-// after the pass loop, so the planes' registers are free for it.
-// st: solved, guesses, sweeps (wave-uniform).
-template <class IO>
-__device__ __forceinline__ void plane_tail(PackLds &W, int lane, uint64_t act, uint32_t p_lo, uint32_t p_hi,
-                                        const IO &io, unsigned long long *__restrict__ ws,
-                                        const int64_t *best, int order, uint32_t (&st)[3])
-{
-    PCells cs;
-    pinit_lane(cs, lane);
-    uint32_t solved = 0, guesses = 0, sweeps = 0;
-    while (act) {
-        const int i = __builtin_ctzll(act);
-        act &= act - 1;
-        const int64_t pi = ((int64_t)rdlane(p_hi, i) << 32) | rdlane(p_lo, i);
-        psolve_board(W, lane, cs, io.b_in(pi), io.b_out(pi), io.b_st(pi), io.local(pi), ws, best, order, solved,
-                     guesses, sweeps);
-    }
-    st[0] = solved;
-    st[1] = guesses;
-    st[2] = sweeps;
-}
-
 // ---- cooperative span loads through LDS
 // A refill (and the start-up) takes k <= 64 CONSECUTIVE boards from the
 // queue, i.e. one contiguous byte span of the batch.  It lands in the wave's
@@ -512,8 +471,6 @@ __device__ __forceinline__ void plane_flush_outbox(const uint32_t *outbox, uint3
 enum { PLANE_TAIL_REC = 33, PLANE_TAIL_MAX = 40 };  // word 32: the board's search mode (mst)
 // the last record, read up to word 48 (pad lanes), stays below the zero byte
 static_assert((PLANE_TAIL_MAX - 1) * PLANE_TAIL_REC + 48 < PLANE_STAGE_DWORDS - 1, "tail records");
-// a pool record's word 33: the board's split descriptor + 1 (0: a whole board)
-enum { PLANE_REC_DESC = 33 };
 
 // The board's stack in the wide layout: lane 16b+d owns word 3d+b of each
 // level's line; the branch entry (word 27) goes through lane 48 (a pad lane)
@@ -541,18 +498,6 @@ struct WideStack {
     __device__ __forceinline__ void put_entry(uint32_t level, uint32_t e) const
     {
         if (__lane_id() == 0) __builtin_amdgcn_raw_buffer_store_b32(e, rsrc, (int)(lane_off + level * 128u + 108u), 0, 0);
-    }
-    // the levels below `depth` that still hold an untried digit (bit l: level
-    // l), all entries in one round trip (lane l reads level l's), and the
-    // entry of the shallowest one
-    __device__ __forceinline__ uint64_t open_levels(uint32_t depth, uint32_t &first) const
-    {
-        const uint32_t l = __lane_id();
-        const uint32_t e =
-            l < depth ? __builtin_amdgcn_raw_buffer_load_b32(rsrc, (int)(lane_off + l * 128u + 108u), 0, 0) : 0u;
-        const uint64_t m = __builtin_amdgcn_ballot_w64(((e >> 8) & 0x1FFu) != 0u);
-        first = m ? rdlane(e, __builtin_ctzll(m)) : 0u;
-        return m;
     }
 };
 
@@ -621,53 +566,17 @@ __device__ __forceinline__ void plane_wide_answer(int r, uint32_t w, int64_t pb,
 // one a producer has reserved and is writing or has written.  (A
 // compare-and-swap on the head, 128 waves per XCD racing, measured 66 failed
 // swaps per record and a 25x slower launch.)
-//
-// Split counting.  A board that reaches the pool in the
-// completion count (M_COUNT, plane::search_step) can be the one that ends
-// the launch: up to ~1000 wide passes.  Its subtrees are independent in
-// that mode, so while other waves of the XCD wait for work (`hungry`), the
-// wave solving it deals the untried digits of its shallowest open stack
-// level out as pool records of their own -- the in-launch analogue of the
-// reference's per-board peer split (node.py:427-449).  The board then has a
-// descriptor: subtrees still running (`outstanding`), completions found
-// (capped use: 0, 1, or "several"), the first completion's planes and the
-// count's root planes.  The wave that ends the last subtree answers the
-// board: no completion -> none, one -> it (the walk's first, being the only
-// one), several (or a count too deep for a stack) -> the walk from the root
-// (M_FINAL), which is never split.  Waves wait for work only while some
-// count-mode board is being solved from the pool (`counting`), so the wait
-// ends once every such board has.
 #ifndef SDK_PLANE_POOL_INV
 #define SDK_PLANE_POOL_INV 1
 #endif
-// default split policy (kernel argument; $SDK_PLANE_SPLIT): 0 off, 1 while
-// waves wait for work, 2 at every opportunity (tests: the most splits)
-#ifndef SDK_PLANE_SPLIT
-#define SDK_PLANE_SPLIT 0
-#endif
-// guess points between two looks at the `hungry` word (split policy 1)
-#ifndef SDK_PLANE_SPLIT_EVERY
-#define SDK_PLANE_SPLIT_EVERY 8
-#endif
-// (the waiting waves poll COUNTING / HUNGRY: a line of their own, so the
-// polls do not queue in front of the claims' atomics on the first one)
-enum {
-    POOL_RESERVED = 0, POOL_AVAIL = 1, POOL_HEAD = 2, POOL_DESC_NEXT = 3,
-    POOL_COUNTING = 32, POOL_HUNGRY = 33,
-    POOL_LANE_LIVE = 34  // waves still in their lane loop (policy 4: they may hand boards over)
-};
-static_assert(POOL_DESC_NEXT < 4 && POOL_HUNGRY < 36, "pool control words re-armed per call (arm_kernel)");
-// descriptor words: subtrees outstanding, completions, walk needed, board id
-// lo / hi; the first completion's planes at DESC_FOUND + 3d+b, the root's at
-// DESC_ROOT + 3d+b
-enum { DESC_OUT = 0, DESC_COMPL = 1, DESC_WALK = 2, DESC_ID = 3, DESC_FOUND = 8, DESC_ROOT = 36 };
-static_assert(DESC_ROOT + 27 <= PLANE_POOL_DESC_WORDS, "descriptor layout");
+// control words of an XCD's pool (one 128-byte line, re-armed per call by arm_kernel)
+enum { POOL_RESERVED = 0, POOL_AVAIL = 1, POOL_HEAD = 2 };
+static_assert(POOL_HEAD < PLANE_POOL_ARM_WORDS, "pool control words re-armed per call (arm_kernel)");
 
 struct PlanePool {
-    uint32_t *ctl;       // the control words (POOL_*)
-    uint32_t *recs;      // PLANE_POOL_CAP records of PLANE_POOL_REC dwords
-    uint32_t *flags;     // the generation of the launch that published the record
-    uint32_t *descs;     // PLANE_POOL_DESCS descriptors of PLANE_POOL_DESC_WORDS dwords
+    uint32_t *ctl;    // the control words (POOL_*)
+    uint32_t *recs;   // PLANE_POOL_CAP records of PLANE_POOL_REC dwords
+    uint32_t *flags;  // the generation of the launch that published the record
     __device__ __forceinline__ int32_t *word(int k) const { return (int32_t *)(ctl + k); }
 };
 
@@ -677,11 +586,10 @@ __device__ __forceinline__ PlanePool plane_pool(int64_t *defer_list)
     const uint32_t x = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | 20) & (PLANE_POOL_XCDS - 1);
     uint32_t *base = (uint32_t *)(defer_list + PLANE_DEFER_CAP) + (size_t)x * PLANE_POOL_STRIDE;
     uint32_t *recs = base + PLANE_POOL_CTL;
-    uint32_t *flags = recs + (size_t)PLANE_POOL_CAP * PLANE_POOL_REC;
-    return {base, recs, flags, flags + PLANE_POOL_CAP};
+    return {base, recs, recs + (size_t)PLANE_POOL_CAP * PLANE_POOL_REC};
 }
 
-// wave-uniform agent-scope atomics on lane 0
+// wave-uniform agent-scope atomic on lane 0
 __device__ __forceinline__ int32_t pool_add(int32_t *p, int32_t v)
 {
     int32_t r = 0;
@@ -706,122 +614,39 @@ __device__ __forceinline__ void pool_publish(const PlanePool &pool, uint32_t s0,
     pool_add(pool.word(POOL_AVAIL), (int32_t)k);
 }
 
-// wide::solve's hooks over the pool (plane_wide.h NoSplit for the contract)
-struct PoolHook {
-    const PlanePool &pool;
-    unsigned long long *ws;
+// wide::solve's hook: ordered mode, a lower board has a completion
+struct CancelHook {
     const int64_t *best;
-    int64_t pb;          // the board
-    uint32_t gen;
-    int mode;            // split policy: 0 off, 1 while waves wait, 2 always
-    uint32_t *desc;      // the board's split descriptor (null: whole board)
-    uint32_t desc_idx;
-    bool counted;        // this wave counts in the pool's `counting` (every increment is undone by this wave)
-    uint32_t looks;      // guess points since the last look at `hungry`
-    uint32_t sol_level;  // the whole board's kept-completion level
+    int64_t pb;  // the board
     __device__ __forceinline__ bool cancelled() const
     {
         return best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pb;
     }
-    __device__ __forceinline__ void counting(bool on)
-    {
-        if (on == counted || (on && !mode)) return;
-        pool_add(pool.word(POOL_COUNTING), on ? 1 : -1);
-        counted = on;
-    }
-    __device__ __forceinline__ bool split() const { return desc != nullptr; }
-    __device__ __forceinline__ bool completion(uint32_t w)
-    {
-        const int32_t c = pool_add((int32_t *)desc + DESC_COMPL, 1);
-        if (c == 0) {  // the board's first: its planes kept in the descriptor
-            const wide::Lanes L = wide::lanes();
-            if (L.valid) desc[DESC_FOUND + L.word] = w;
-        }
-        return c == 0;
-    }
-    __device__ __forceinline__ bool abandoned()
-    {
-        if ((++looks & 7u) != 0u) return false;  // an atomic load every few guesses (bit 31: no split)
-        return pool_load((const int32_t *)desc + DESC_COMPL) >= 2 || pool_load((const int32_t *)desc + DESC_WALK) != 0;
-    }
-    __device__ __forceinline__ void need_walk()
-    {
-        if (__lane_id() == 0) __hip_atomic_store(desc + DESC_WALK, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    template <class Stack>
-    __device__ __forceinline__ void try_split(uint32_t w, uint32_t depth, uint32_t &mst, const Stack &stk,
-                                              const wide::Lanes &L)
-    {
-        if (!mode || mode >= 3 || depth == 0 || (looks >> 31)) return;  // (3, 4: waves wait, no deals)
-        if (mode == 1) {
-            if ((++looks % SDK_PLANE_SPLIT_EVERY) != 0u) return;
-            if (pool_load(pool.word(POOL_HUNGRY)) <= 0) return;
-        }
-        uint32_t e = 0;
-        const uint64_t open = stk.open_levels(depth, e);
-        if (!open) return;
-        const uint32_t lvl = (uint32_t)__builtin_ctzll(open);
-        const uint32_t rem = (e >> 8) & 0x1FFu;
-        if (!desc) {
-            // the board's descriptor: one subtree (this one), its root, and a
-            // completion this search has already kept
-            const int32_t d = pool_add(pool.word(POOL_DESC_NEXT), 1);
-            if (d >= PLANE_POOL_DESCS) {
-                looks = 1u << 31;  // none left: this board stays whole
-                return;
-            }
-            uint32_t *D = pool.descs + (size_t)d * PLANE_POOL_DESC_WORDS;
-            const bool found = (mst & plane::MST_FOUND) != 0;
-            const uint32_t root = stk.restore(0, L);
-            const uint32_t kept = found ? stk.restore(sol_level, L) : 0u;
-            if (L.valid) {
-                D[DESC_ROOT + L.word] = root;
-                if (found) D[DESC_FOUND + L.word] = kept;
-            }
-            if (__lane_id() == 0) {
-                D[DESC_OUT] = 1u;
-                D[DESC_COMPL] = found ? 1u : 0u;
-                D[DESC_WALK] = 0u;
-                D[DESC_ID] = (uint32_t)pb;
-                D[DESC_ID + 1] = (uint32_t)(pb >> 32);
-            }
-            __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // in L2 before any subtree of it can end
-            mst &= ~plane::MST_FOUND;
-            desc = D;
-            desc_idx = (uint32_t)d;
-        }
-        // the level's untried digits, one pool record each
-        const uint32_t k = (uint32_t)__builtin_popcount(rem);
-        const uint32_t s0 = (uint32_t)pool_add(pool.word(POOL_RESERVED), (int32_t)k);
-        const uint32_t fit = s0 >= PLANE_POOL_CAP ? 0u : (PLANE_POOL_CAP - s0 < k ? PLANE_POOL_CAP - s0 : k);
-        if (!fit) return;
-        pool_add((int32_t *)desc + DESC_OUT, (int32_t)fit);  // counted before any of them can end
-        const uint32_t base = stk.restore(lvl, L);
-        const int band = (int)((e >> 5) & 3u), pos = (int)(e & 31u);
-        uint32_t left = rem;
-        for (uint32_t i = 0; i < fit; ++i) {
-            const uint32_t dbit = left & (0u - left);
-            left ^= dbit;
-            uint32_t c = base;
-            wide::set_cell(c, L, band, pos, dbit);
-            uint32_t *rec = pool.recs + (size_t)(s0 + i) * PLANE_POOL_REC;
-            if (L.valid) rec[L.word] = c;
-            const uint32_t hdr = __lane_id() == 0 ? (uint32_t)pb
-                               : __lane_id() == 1 ? (uint32_t)(pb >> 32)
-                               : __lane_id() == 5 ? plane::mst_set_mode(0u, plane::M_COUNT)
-                               : __lane_id() == 6 ? desc_idx + 1u
-                                                  : 0u;
-            if (__lane_id() < 9) rec[27 + __lane_id()] = hdr;  // id, depth 0, stack (own), guesses, mode, descriptor
-        }
-        stk.put_entry(lvl, e & ~((rem ^ left) << 8));  // the dealt digits leave this level
-        pool_publish(pool, s0, fit, gen, (int)__lane_id());
-        if (__lane_id() == 0) atomicAdd(&ws[WS_SPLITS], 1ull);
-    }
 };
 
-// Solve the k boards recorded in `recs` on the wave-wide solver, one after
-// the other (a wave's own tail: no splitting).  st: solved, guesses (net of
+// Continue board pb (this lane's plane word w, its search state as the tail
+// record holds it: depth, stack line, guesses so far, search mode) on the
+// wave-wide solver and write its answer.  st: solved, guesses (net of
 // deferred boards'), passes, deferred, answered -- wave-uniform.
+template <class IO>
+__device__ __forceinline__ void plane_wide_record(uint32_t w, int64_t pb, uint32_t depth, uint32_t stack_off,
+                                                  uint32_t bguess, uint32_t mst, const wide::Lanes &L, int lane,
+                                                  __amdgpu_buffer_rsrc_t stack_rsrc, const IO &io,
+                                                  unsigned long long *__restrict__ ws, int64_t *__restrict__ defer_list,
+                                                  const int64_t *best, int node_order, uint32_t mrv_after,
+                                                  uint32_t (&st)[5])
+{
+    const WideStack stk = {stack_rsrc, stack_off, L.valid ? 4u * L.word : 108u, L.valid, lane == 48};
+    wide::Stats ws_ = {0u, 0u, bguess};
+    CancelHook hk = {best, pb};
+    const int r = wide::solve(w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_, hk, mst, mrv_after);
+    st[2] += ws_.passes;
+    st[1] += ws_.guesses;
+    plane_wide_answer(r, w, pb, ws_.bguess, lane, L, io, ws, defer_list, best, st);
+}
+
+// Solve the k boards recorded in `recs` on the wave-wide solver, one after
+// the other (a wave's own tail).  st as plane_wide_record's.
 template <class IO>
 __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
                                              const IO &io, unsigned long long *__restrict__ ws,
@@ -829,78 +654,41 @@ __device__ __forceinline__ void plane_wide_tail(const uint32_t *recs, int k, int
                                              uint32_t mrv_after, uint32_t (&st)[5])
 {
     const wide::Lanes L = wide::lanes();
-    const PlanePool pool = plane_pool(defer_list);
     for (int s = 0; s < k; ++s) {
         const uint32_t *rec = recs + PLANE_TAIL_REC * s;
         uint32_t w = rec[L.valid ? L.word : 0u];
         w = L.valid ? w : 0u;
         const int64_t pb = ((int64_t)__builtin_amdgcn_readfirstlane(rec[28]) << 32) |
                            (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane(rec[27]);
-        uint32_t depth = __builtin_amdgcn_readfirstlane(rec[29]);
-        const WideStack stk = {stack_rsrc, (uint32_t)__builtin_amdgcn_readfirstlane(rec[30]),
-                               L.valid ? 4u * L.word : 108u, L.valid, lane == 48};
-        wide::Stats ws_ = {0u, 0u, (uint32_t)__builtin_amdgcn_readfirstlane(rec[31])};
-        uint32_t mst = __builtin_amdgcn_readfirstlane(rec[32]);
-        PoolHook hk = {pool, ws, best, pb, 0u, 0, nullptr, 0u, false, 0u, PLANE_MAX_DEPTH - 1};
-        const int r = wide::solve(w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_, hk, mst, mrv_after);
-        st[2] += ws_.passes;
-        st[1] += ws_.guesses;
-        plane_wide_answer(r, w, pb, ws_.bguess, lane, L, io, ws, defer_list, best, st);
+        plane_wide_record(w, pb, __builtin_amdgcn_readfirstlane(rec[29]), __builtin_amdgcn_readfirstlane(rec[30]),
+                          __builtin_amdgcn_readfirstlane(rec[31]), __builtin_amdgcn_readfirstlane(rec[32]), L, lane,
+                          stack_rsrc, io, ws, defer_list, best, node_order, mrv_after, st);
     }
 }
 
-// Take records from the pool until it is empty and no count-mode board is
-// being solved from it (wave-uniform).  A taken slot has a producer that
-// reserved it and writes it without waiting on anything, so the flag wait is
-// short (a flag holds the launch generation `gen`, so a flag an earlier
-// launch left never reads as set).  It is bounded all the same (`polls`
-// polls, ~1 s by default): a wave that gives up sets SDK_ERR_POOL_WAIT in the
-// workspace -- that record's board is not answered, and sdk_verify_workspace
-// turns the word into a failed call -- and leaves the pool.  own_off: a stack
-// of this wave's no other wave uses (split subtrees, the walk of a split
-// board).  split: the split policy.
+// Take records from the pool until none is published (wave-uniform).  A
+// taken slot has a producer that reserved it and writes it without waiting
+// on anything, so the flag wait is short (a flag holds the launch generation
+// `gen`, so a flag an earlier launch left never reads as set).  It is bounded
+// all the same (`polls` polls, ~1 s by default): a wave that gives up sets
+// SDK_ERR_POOL_WAIT in the workspace -- that record's board is not answered,
+// and sdk_verify_workspace turns the word into a failed call -- and leaves
+// the pool.  st as plane_wide_record's.
 template <class IO>
-__device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t *stage, int lane,
-                                              __amdgpu_buffer_rsrc_t stack_rsrc, uint32_t own_off, const IO &io,
-                                              unsigned long long *__restrict__ ws, int64_t *__restrict__ defer_list,
-                                              const int64_t *best, int node_order, uint32_t mrv_after,
-                                              uint32_t gen, uint32_t polls, int split, uint32_t (&st)[5])
+__device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
+                                              const IO &io, unsigned long long *__restrict__ ws,
+                                              int64_t *__restrict__ defer_list, const int64_t *best, int node_order,
+                                              uint32_t mrv_after, uint32_t gen, uint32_t polls, uint32_t (&st)[5])
 {
-    (void)stage;
 #if SDK_PLANE_STAMPS
     // diagnostic: claims, backed-out claims, flag polls; cycles claiming, waiting, solving (ws words 24..29)
     uint64_t d_ok = 0, d_fail = 0, d_poll = 0, c_claim = 0, c_wait = 0, c_solve = 0;
     uint64_t d_t = __builtin_amdgcn_s_memtime();
 #endif
     const wide::Lanes L = wide::lanes();
-    if (best) split = 0;  // ordered mode: the lowest board decides, no count is shared
-    bool waiting = false;  // counted in `hungry`
-    uint32_t idle = 0;     // polls spent waiting (bounded: a count-mode board ends in well under 2 ms)
-    // (a waiting wave polls AVAIL and COUNTING every ~1.7 us: 512 waves of an
-    // XCD polling every 0.2 us queued the claims' atomics behind them)
-    for (;;) {
-        if (pool_load(pool.word(POOL_AVAIL)) <= 0) {
-            // nothing published: wait only while a count-mode board is being
-            // solved from the pool (it may deal out subtrees)
-            if (!split || (pool_load(pool.word(POOL_COUNTING)) <= 0 &&
-                           (split != 4 || pool_load(pool.word(POOL_LANE_LIVE)) <= 0)))
-                break;
-            if (++idle > (1u << 13)) {
-                // ~0.25 s: no board takes that long; a leaked count would hang
-                // the launch, so leave (every record is still taken: a
-                // publishing wave drains its own before it exits) and say so
-                if (lane == 0) atomicOr(&ws[WS_ERROR], (unsigned long long)SDK_ERR_POOL_IDLE);
-                break;
-            }
-            if (!waiting) {
-                pool_add(pool.word(POOL_HUNGRY), 1);
-                waiting = true;
-            }
-            // back off: 1.7 us doubling to ~27 us between polls (a wave's
-            // polls must not crowd the L2 channel the solving waves use)
-            for (uint32_t k = 0; k < (1u << (idle < 4 ? idle : 4)); ++k) __builtin_amdgcn_s_sleep(64);
-            continue;
-        }
+    while (pool_load(pool.word(POOL_AVAIL)) > 0) {
+        // take one of the PUBLISHED records: decrement `avail` (putting the
+        // unit back if it was already used up), then draw the slot
         uint32_t h = 0;
         int32_t a = 0;
         if (lane == 0) {
@@ -917,10 +705,6 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
             continue;  // another wave took the last one: look again
         }
         h = __builtin_amdgcn_readfirstlane(h);
-        if (waiting) {
-            pool_add(pool.word(POOL_HUNGRY), -1);
-            waiting = false;
-        }
 #if SDK_PLANE_STAMPS
         d_ok++;
         {
@@ -965,49 +749,8 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
         uint32_t w = __builtin_amdgcn_ds_bpermute((int)(4u * (L.valid ? L.word : 0u)), (int)rw);
         w = L.valid ? w : 0u;
         const int64_t pb = ((int64_t)rdlane(rw, 28) << 32) | (int64_t)rdlane(rw, 27);
-        uint32_t depth = rdlane(rw, 29);
-        const uint32_t di = rdlane(rw, PLANE_REC_DESC);  // a split subtree: its board's descriptor + 1
-        const WideStack stk = {stack_rsrc, di ? own_off : rdlane(rw, 30), L.valid ? 4u * L.word : 108u, L.valid,
-                               lane == 48};
-        wide::Stats ws_ = {0u, 0u, rdlane(rw, 31)};
-        uint32_t mst = rdlane(rw, 32);
-        PoolHook hk = {pool, ws, best, pb, gen, split,
-                       di ? pool.descs + (size_t)(di - 1) * PLANE_POOL_DESC_WORDS : nullptr, di ? di - 1 : 0u, false, 0u,
-                       PLANE_MAX_DEPTH - 1};
-        hk.counting(plane::mst_mode(mst) == plane::M_COUNT);
-        int r = wide::solve(w, depth, stk, L, node_order, PLANE_MAX_DEPTH, ws_, hk, mst, mrv_after);
-        hk.counting(false);
-        st[2] += ws_.passes;
-        st[1] += ws_.guesses;
-        if (r != wide::W_SUBTREE) {
-            plane_wide_answer(r, w, pb, ws_.bguess, lane, L, io, ws, defer_list, best, st);
-        } else {
-            // this share of a split board's count is done; the last one answers the board
-            __builtin_amdgcn_s_waitcnt(SDK_WAIT_VM0);  // this share's completion (if any) is in L2
-            uint32_t *D = hk.desc;
-            if (pool_add((int32_t *)D + DESC_OUT, -1) == 1) {
-                const int32_t c = pool_load((const int32_t *)D + DESC_COMPL);
-                const bool walk = c >= 2 || pool_load((const int32_t *)D + DESC_WALK) != 0;
-                const uint32_t x = L.valid ? __hip_atomic_load(D + (walk ? DESC_ROOT : DESC_FOUND) + L.word,
-                                                              __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                           : 0u;
-                w = L.valid ? x : 0u;
-                if (walk) {
-                    // several completions (or too deep to count): the walk
-                    // decides, from the count's root, on this wave's own stack
-                    const WideStack own = {stack_rsrc, own_off, L.valid ? 4u * L.word : 108u, L.valid, lane == 48};
-                    uint32_t d0 = 0, m0 = plane::mst_set_mode(0u, plane::M_FINAL);
-                    wide::Stats wf = {0u, 0u, 0u};
-                    PoolHook hf = {pool, ws, best, pb, gen, 0, nullptr, 0u, false, 0u, PLANE_MAX_DEPTH - 1};
-                    r = wide::solve(w, d0, own, L, node_order, PLANE_MAX_DEPTH, wf, hf, m0, mrv_after);
-                    st[2] += wf.passes;
-                    st[1] += wf.guesses;
-                } else {
-                    r = c == 1 ? wide::W_SOLVED : wide::W_UNSOLVABLE;
-                }
-                plane_wide_answer(r, w, pb, 0u, lane, L, io, ws, defer_list, best, st);
-            }
-        }
+        plane_wide_record(w, pb, rdlane(rw, 29), rdlane(rw, 30), rdlane(rw, 31), rdlane(rw, 32), L, lane, stack_rsrc,
+                          io, ws, defer_list, best, node_order, mrv_after, st);
 #if SDK_PLANE_STAMPS
         {
             const uint64_t t1 = __builtin_amdgcn_s_memtime();
@@ -1016,7 +759,6 @@ __device__ __forceinline__ void plane_pool_drain(const PlanePool &pool, uint32_t
         }
 #endif
     }
-    if (waiting) pool_add(pool.word(POOL_HUNGRY), -1);
 #if SDK_PLANE_STAMPS
     c_claim += __builtin_amdgcn_s_memtime() - d_t;
     if (lane == 0) {
@@ -1038,311 +780,6 @@ __device__ __forceinline__ uint32_t wave_sum(uint32_t v)
     return v;
 }
 
-// ---- the tail pool on the four-board solver (tail mode 3, plane_quad.h)
-enum { Q_SEARCHING = -100 };  // a row's answer while it has none (wide::W_* are -1..3)
-// Claim one published record (wave-uniform): 1 and its slot in h, 0 if none
-// is published, -1 if its flag never came (SDK_ERR_POOL_WAIT set).
-__device__ __forceinline__ int pool_claim(const PlanePool &pool, unsigned long long *__restrict__ ws, uint32_t gen,
-                                          uint32_t polls, uint32_t &h)
-{
-    for (;;) {
-        if (pool_load(pool.word(POOL_AVAIL)) <= 0) return 0;
-        int32_t a = 0;
-        uint32_t s = 0;
-        if (__lane_id() == 0) {
-            a = __hip_atomic_fetch_add(pool.word(POOL_AVAIL), -1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (a > 0)
-                s = __hip_atomic_fetch_add(pool.ctl + POOL_HEAD, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            else
-                __hip_atomic_fetch_add(pool.word(POOL_AVAIL), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        if (__builtin_amdgcn_readfirstlane(a) <= 0) continue;  // another wave took the last one: look again
-        h = __builtin_amdgcn_readfirstlane(s);
-        for (uint32_t tries = 0; tries < polls; ++tries) {
-            uint32_t f = 0;
-            if (__lane_id() == 0) f = __hip_atomic_load(pool.flags + h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (__builtin_amdgcn_readfirstlane(f) == gen) {
-#if SDK_PLANE_POOL_INV == 2
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-#elif SDK_PLANE_POOL_INV == 1
-                asm volatile("buffer_inv sc0" ::: "memory");  // this CU's L1 only
-#endif
-                return 1;
-            }
-            __builtin_amdgcn_s_sleep(2);
-        }
-        if (__lane_id() == 0) {
-            atomicOr(&ws[WS_ERROR], (unsigned long long)SDK_ERR_POOL_WAIT);
-            __hip_atomic_store(&ws[WS_ERR_SLOT], (unsigned long long)h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-        return -1;
-    }
-}
-
-// Drain the XCD's pool four boards at a time: row q of the wave (lanes
-// 16q..16q+15) holds one board, lane 16q+d its digit d's three band words,
-// and its stack is the record's (the donor lane's lines: word 3d+b of a
-// level's line is P[d][b], so a lane moves its 12 bytes; the branch entry,
-// word 27, goes through the row's lane d = 9).  Every iteration runs one
-// pass over all four rows (full wave: the row sums are DPP), then each row's
-// search step -- the transitions of wide::solve / plane::search_step, per
-// row under its own exec mask (the cross-lane parts -- fewest-candidates
-// counts, candidate ballots -- run for all rows before it).  A row whose
-// board has its answer writes it (plane_wide_answer, after a move to the
-// wide layout) and takes the next record.  st as plane_wide_tail's.
-template <class IO>
-__device__ __forceinline__ void plane_quad_drain(const PlanePool &pool, int lane, __amdgpu_buffer_rsrc_t stack_rsrc,
-                                              const IO &io, unsigned long long *__restrict__ ws,
-                                              int64_t *__restrict__ defer_list, const int64_t *best, int node_order,
-                                              uint32_t mrv_after, uint32_t gen, uint32_t polls, uint32_t (&st)[5])
-{
-    const quad::Lanes QL = quad::lanes();
-    const wide::Lanes WL = wide::lanes();
-    const uint32_t row = (uint32_t)lane >> 4, dg = (uint32_t)lane & 15u;
-    const bool valid = dg < 9u;
-    const uint32_t max_depth = PLANE_MAX_DEPTH, sol_level = PLANE_MAX_DEPTH - 1;
-    // per lane; all but w row-uniform
-    uint32_t w[3] = {0u, 0u, 0u}, det[3] = {0u, 0u, 0u}, und[3] = {0u, 0u, 0u};
-    uint32_t depth = 0, mst = 0, sbase = 0, bguess = 0;
-    int64_t pb = 0;
-    bool busy = false;
-    uint32_t n_pass = 0, n_guess = 0;  // counted once per row (lane d = 0)
-    bool pool_empty = false;  // the last claim found nothing (retried every 8 iterations)
-    uint32_t iter = 0;
-    // the row's stack accesses: this lane's 12 bytes of a level's line, the entry word
-    auto ld3 = [&](uint32_t level, uint32_t (&x)[3]) {
-        const int o = (int)(sbase + level * 128u + 12u * dg);
-#pragma unroll
-        for (int b = 0; b < 3; ++b) x[b] = valid ? __builtin_amdgcn_raw_buffer_load_b32(stack_rsrc, o + 4 * b, 0, 0) : 0u;
-    };
-    auto st3 = [&](uint32_t level, const uint32_t (&x)[3], uint32_t entry) {
-        const int o = (int)(sbase + level * 128u + 12u * dg);
-        if (valid) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b) __builtin_amdgcn_raw_buffer_store_b32(x[b], stack_rsrc, o + 4 * b, 0, 0);
-        } else if (dg == 9u) {
-            __builtin_amdgcn_raw_buffer_store_b32(entry, stack_rsrc, (int)(sbase + level * 128u + 108u), 0, 0);
-        }
-    };
-    auto ld_entry = [&](uint32_t level) {
-        return __builtin_amdgcn_raw_buffer_load_b32(stack_rsrc, (int)(sbase + level * 128u + 108u), 0, 0);
-    };
-    for (uint32_t guard = 0;; ++guard) {
-        if (guard > (1u << 22)) {  // ~4 M passes: no board needs that; leave loudly rather than hang
-            if (lane == 0) atomicOr(&ws[WS_ERROR], (unsigned long long)SDK_ERR_QUAD_STALL);
-            if (lane < 4) {  // diagnostic: each row's state
-                const int l = 16 * lane;
-                ws[16 + 2 * lane] = ((unsigned long long)rdlane(mst, l) << 32) | rdlane(depth, l);
-                ws[17 + 2 * lane] = ((unsigned long long)rdlane((uint32_t)busy, l) << 32) | rdlane(und[0] | und[1] | und[2], l);
-            }
-            break;
-        }
-        // ---- refill the idle rows from the pool (other waves may still publish)
-        uint64_t bm = __builtin_amdgcn_ballot_w64(busy);
-        if (pool_empty && (++iter & 7u) == 0u) pool_empty = false;
-        for (uint32_t q = 0; q < 4u && !pool_empty; ++q) {
-            if ((bm >> (16u * q)) & 1u) continue;
-            uint32_t h = 0;
-            const int c = pool_claim(pool, ws, gen, polls, h);
-            if (c <= 0) {
-                pool_empty = true;  // (a failed flag wait leaves too: the error word says so)
-                break;
-            }
-            const uint32_t *rec = pool.recs + (size_t)h * PLANE_POOL_REC;
-            const uint32_t rw = lane < PLANE_POOL_REC
-                                    ? __hip_atomic_load(rec + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
-                                    : 0u;
-            uint32_t x[3];
-#pragma unroll
-            for (int b = 0; b < 3; ++b)
-                x[b] = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4u * (valid ? 3u * dg + b : 0u)), (int)rw);
-            const int64_t qb = ((int64_t)rdlane(rw, 28) << 32) | (int64_t)rdlane(rw, 27);
-            const uint32_t qd = rdlane(rw, 29), qs = rdlane(rw, 30), qg = rdlane(rw, 31), qm = rdlane(rw, 32);
-            if (row == q) {
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    w[b] = valid ? x[b] : 0u;
-                    det[b] = 0u;
-                }
-                pb = qb;
-                depth = qd;
-                sbase = qs;
-                bguess = qg;
-                mst = qm;
-                busy = true;
-            }
-            bm |= 1ull << (16u * q);
-        }
-        if (!bm) {
-            if (!pool_empty) continue;  // (cannot happen: an idle wave claims until empty)
-            break;                      // no board left here and none published
-        }
-
-        // ---- one pass over the four rows (all lanes: the row sums are DPP)
-        const uint32_t r0 = quad::pass(w, det, und, QL);
-        if (busy && dg == 0u) n_pass++;
-
-        // ---- the search step's decisions (row-uniform per lane)
-        int r = busy ? (int)r0 : quad::OPEN;
-        mst += busy ? 1u : 0u;
-        int mode = plane::mst_mode(mst);
-        if (busy && r == quad::STUCK && plane::root_counts(mode, depth, mrv_after, und[0], und[1], und[2])) {
-            mode = plane::M_COUNT;  // a wide-open root: count at once (plane::search_step)
-            mst = plane::mst_set_mode(mst, plane::M_COUNT);
-        }
-        int res = Q_SEARCHING;  // the row's answer (wide::W_*; W_OVERFLOW is -1)
-        int reload = -1;       // a level whose planes replace the row's board
-        bool scan = false;     // reload scans down for an untried digit
-        bool guess = false, push_sol = false;
-        if (busy && mode == plane::M_WALK && mrv_after && r != quad::SOLVED && (mst & plane::MST_PASSES) >= mrv_after) {
-            reload = depth ? 0 : -1;  // the propagated root
-            depth = 0;
-            mst = plane::mst_set_mode(mst, plane::M_COUNT);
-            r = quad::OPEN;
-            if (reload < 0)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) det[b] = 0u;
-        }
-        if (r == quad::SOLVED) {
-            if (mode != plane::M_COUNT) {
-                res = wide::W_SOLVED;
-            } else if (mst & plane::MST_FOUND) {  // a second completion: the walk, from the root
-                reload = 0;
-                depth = 0;
-                mst = plane::mst_set_mode(mst, plane::M_FINAL);
-            } else {
-                mst |= plane::MST_FOUND;
-                push_sol = true;
-                r = quad::DEAD;  // and look for another
-            }
-        }
-        if (r == quad::STUCK) {
-            if (depth == (mode == plane::M_COUNT ? sol_level : max_depth)) {
-                if (mode != plane::M_COUNT) {
-                    res = wide::W_OVERFLOW;
-                } else {
-                    reload = 0;  // too deep to count: the walk, from the root
-                    depth = 0;
-                    mst = plane::mst_set_mode(mst, plane::M_FINAL);
-                }
-            } else if (best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < pb) {
-                res = wide::W_CANCELLED;
-            } else {
-                guess = true;
-            }
-        }
-        if (r == quad::DEAD) {
-            if (depth) {
-                scan = true;
-                reload = (int)depth - 1;
-            } else if (mode == plane::M_COUNT && (mst & plane::MST_FOUND)) {
-                reload = push_sol ? -1 : (int)sol_level;  // exactly one completion (w is it if just found)
-                res = wide::W_SOLVED;
-            } else {
-                res = wide::W_UNSOLVABLE;
-            }
-        }
-        // ---- the branch cell of the rows that guess (cross-lane: every lane takes part)
-        int band = 0, pos = 0;
-        uint32_t cand = 0;
-        const uint64_t gm = __builtin_amdgcn_ballot_w64(guess);
-        if (gm) {
-            // (the picks only in the guessing rows: they take ctz / clz of
-            // undetermined-cell words, which are 0 in a solved row)
-            if (__builtin_amdgcn_ballot_w64(guess && mode == plane::M_COUNT)) {
-                uint32_t e2[3], e3[3];
-#pragma unroll
-                for (int b = 0; b < 3; ++b) {
-                    uint32_t t, th, f;
-                    wide::row_count234(valid ? w[b] : 0u, t, th, f);
-                    e2[b] = und[b] & plane::andn(t, th);
-                    e3[b] = und[b] & plane::andn(th, f);
-                }
-                if (guess && mode == plane::M_COUNT) plane::pick_mrv_masks(e2, e3, und, band, pos);
-                else if (guess) plane::pick_cell(und, node_order, band, pos);
-            } else if (guess) {
-                plane::pick_cell(und, node_order, band, pos);
-            }
-            const uint32_t wb = band == 0 ? w[0] : band == 1 ? w[1] : w[2];
-            const uint64_t cm = __builtin_amdgcn_ballot_w64(guess && valid && ((wb >> pos) & 1u));
-            cand = (uint32_t)(cm >> (16u * row)) & 0x1FFu;
-        }
-        // ---- the row's own stack work (divergent per row, no cross-lane)
-        uint32_t fix_d = 0;
-        if (push_sol) st3(sol_level, w, 0u);
-        if (guess) {
-            fix_d = cand & (0u - cand);
-            st3(depth, w, plane::make_entry(band, pos, cand ^ fix_d));
-        }
-        if (reload >= 0) {
-#pragma unroll
-            for (int b = 0; b < 3; ++b) det[b] = 0u;
-            while (true) {
-                const uint32_t lv = (uint32_t)reload;
-                if (!scan) {
-                    ld3(lv, w);
-                    break;
-                }
-                const uint32_t e = ld_entry(lv);
-                const uint32_t rem = (e >> 8) & 0x1FFu;
-                if (rem) {
-                    fix_d = rem & (0u - rem);
-                    if (dg == 9u)
-                        __builtin_amdgcn_raw_buffer_store_b32(e & ~(fix_d << 8), stack_rsrc, (int)(sbase + lv * 128u + 108u), 0, 0);
-                    band = (int)((e >> 5) & 3u);
-                    pos = (int)(e & 31u);
-                    depth = lv;
-                    guess = true;  // (the fix below)
-                    ld3(lv, w);
-                    break;
-                }
-                if (lv == 0) {  // exhausted
-                    if (mode == plane::M_COUNT && (mst & plane::MST_FOUND)) {
-                        ld3(sol_level, w);  // exactly one completion
-                        res = wide::W_SOLVED;
-                    } else {
-                        res = wide::W_UNSOLVABLE;
-                    }
-                    break;
-                }
-                reload--;
-            }
-        }
-        if (guess && res == Q_SEARCHING) {
-            depth++;
-            bguess++;
-            if (dg == 0u) n_guess++;
-            // fix the row's cell to the digit: the other digits' lanes drop it
-            if (valid && !((fix_d >> dg) & 1u)) {
-                if (band == 0) w[0] &= ~(1u << pos);
-                else if (band == 1) w[1] &= ~(1u << pos);
-                else w[2] &= ~(1u << pos);
-            }
-        }
-        // ---- rows with an answer write it and take the next board
-        const uint64_t dm = __builtin_amdgcn_ballot_w64(busy && res != Q_SEARCHING);
-        if (dm) {
-            for (uint32_t q = 0; q < 4u; ++q) {
-                if (!((dm >> (16u * q)) & 1u)) continue;
-                // the row's planes in the wide layout (lane 16b+d: P[d][b])
-                const int srcl = (int)(4u * (16u * q + (dg < 9u ? dg : 0u)));
-                const uint32_t x0 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)w[0]);
-                const uint32_t x1 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)w[1]);
-                const uint32_t x2 = (uint32_t)__builtin_amdgcn_ds_bpermute(srcl, (int)w[2]);
-                const uint32_t wb = row == 0 ? x0 : row == 1 ? x1 : x2;
-                const uint32_t ww = WL.valid ? wb : 0u;
-                const int qres = (int)rdlane((uint32_t)res, (int)(16u * q));
-                const int64_t qpb = ((int64_t)rdlane((uint32_t)(pb >> 32), (int)(16u * q)) << 32) |
-                                    (int64_t)rdlane((uint32_t)pb, (int)(16u * q));
-                plane_wide_answer(qres, ww, qpb, rdlane(bguess, (int)(16u * q)), lane, WL, io, ws, defer_list, best, st);
-            }
-            if (busy && res != Q_SEARCHING) busy = false;
-        }
-    }
-    st[2] += wave_sum(n_pass);
-    st[1] += wave_sum(n_guess);
-}
-
 // lane states; the two "original" states store the input board back
 enum { PL_IDLE = 0, PL_ACTIVE = 1, PL_SOLVED = 2, PL_UNSOLVABLE = 3, PL_CANCELLED = 4 };
 
@@ -1361,22 +798,15 @@ template <class IO>
 __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__restrict__ ws,
                                            uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list,
                                            int ordered, int order, int refill, int tail, int tail_mode, int chunk,
-                                           uint32_t mrv_after, uint32_t pool_polls, int split)
+                                           uint32_t mrv_after, uint32_t pool_polls)
 {
-    // (the per-byte deposit path stages one batch segment per claim; only
-    // the converted-records path splits claims at batch boundaries)
-    static_assert(SDK_PLANE_PRECONV || !IO::multi, "SDK_PLANE_PRECONV=0 supports one batch per launch only");
     const int64_t n = io.total();  // boards of the launch (virtual indices 0..n-1)
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ws[WS_ASSIGNED], (unsigned long long)n);  // sdk_verify_workspace
-    __shared__ PackLds tail_lds[PLANE_THREADS / 64];
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     __shared__ __attribute__((aligned(16))) uint32_t outbox_lds[PLANE_THREADS / 64][PLANE_OUTBOX * PLANE_OB_WORDS];
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     uint32_t *outbox = outbox_lds[threadIdx.x >> 6];
     uint32_t ob_count = 0;  // boards waiting in the outbox (wave-uniform)
-#if !SDK_PLANE_PRECONV
-    const uint8_t *stage_b = (const uint8_t *)stage;
-#endif
     if ((threadIdx.x & 63) == 0) stage[PLANE_STAGE_DWORDS - 1] = 0u;  // the zero byte
     const int64_t nt = (int64_t)gridDim.x * PLANE_THREADS;
     const int64_t g = (int64_t)blockIdx.x * PLANE_THREADS + threadIdx.x;
@@ -1404,17 +834,12 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     // refill (the head is one device-scope atomic for 4096 waves).  Chunks
     // shrink towards the end of the batch (guided: remaining / (2 waves)).
     int64_t res_lo = 0, res_hi = 0;
-    int64_t rec_base = 0;  // virtual index of chunk record 0 (SDK_PLANE_PRECONV)
+    int64_t rec_base = 0;  // virtual index of chunk record 0
     int64_t rec_id = 0;    // its board id
     int64_t seg_hi = 0;    // [res_lo, seg_hi) converted (one batch segment), [seg_hi, res_hi) claimed only
     bool queue_out = false;
     const int64_t nwaves = (int64_t)gridDim.x * (PLANE_THREADS / 64);
     uint64_t tail_act = 0;  // lanes whose boards the wave solver restarts after the loop
-    // split policy 4 (steal): this wave counts in its XCD pool's lane-loop waves
-    const bool steal_on = split == 4 && tail_mode >= 2 && !ordered;
-    const PlanePool steal_pool = plane_pool(defer_list);
-    uint32_t steal_chk = 0;
-    if (steal_on) pool_add(steal_pool.word(POOL_LANE_LIVE), 1);
 #if SDK_PLANE_STAMPS
     const uint64_t st_t0 = __builtin_amdgcn_s_memrealtime();
     uint64_t st_t1 = 0;
@@ -1425,7 +850,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     // shader-clock cycles spent in the pass step / the store + refill block /
     // the tail restarts (s_memtime at wave-uniform points)
     uint64_t st_pass = 0, st_io = 0, st_tail = 0, st_tb = 0;
-    uint64_t st_atom = 0, st_dma = 0, st_dep = 0;  // parts of st_io: queue atomic, span DMA, per-board deposit
+    uint64_t st_atom = 0, st_dep = 0;  // parts of st_io: queue atomic, per-board deposit
     uint64_t st_store = 0;                          // part of st_io: storing finished boards
     uint64_t st_claims = 0;                         // queue claims: count | last size << 32
 #endif
@@ -1494,9 +919,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         }
     }
 
-#if SDK_PLANE_ROWS_PERIOD
-    int rows_ctr = 0;
-#endif
     for (;;) {
 #if SDK_PLANE_STAMPS
         const uint64_t st_ta = __builtin_amdgcn_s_memtime();
@@ -1506,9 +928,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             if (!st_t1) st_t1 = __builtin_amdgcn_s_memrealtime();
             st_after++;
         }
-#endif
-#if SDK_PLANE_ROWS_PERIOD
-        rows_ctr = __builtin_amdgcn_readfirstlane(rows_ctr + 1 == SDK_PLANE_ROWS_PERIOD ? 0 : rows_ctr + 1);  // every lane is here
 #endif
         const uint64_t active = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
         if (__builtin_popcountll(~active) >= refill || active == 0) {
@@ -1615,7 +1034,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     res_hi = res_lo + c < n ? res_lo + c : n;
                     if (res_lo > n) res_lo = n;
                     queue_out = res_lo + c >= n;
-#if SDK_PLANE_PRECONV
                     if constexpr (!IO::multi) {
                         // the whole chunk staged and converted once (chunk records)
                         const int cc = __builtin_amdgcn_readfirstlane((int)(res_hi - res_lo));
@@ -1626,11 +1044,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                         }
                     }
                     seg_hi = IO::multi ? res_lo : res_hi;  // (multi: nothing converted yet)
-#else
-                    seg_hi = res_hi;
-#endif
                 }
-#if SDK_PLANE_PRECONV
                 if (IO::multi && res_lo == seg_hi && res_lo < res_hi) {
                     // the claimed chunk staged and converted once (chunk
                     // records), a batch segment at a time (one for one batch)
@@ -1642,7 +1056,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                                                          stage, lane);
                     plane_convert_chunk(stage, sh, cc, lane);
                 }
-#endif
                 base = (unsigned long long)res_lo;
                 // (wave-uniform: readfirstlane keeps the deposit loop a scalar loop)
                 const int64_t avail = (IO::multi ? seg_hi : res_hi) - res_lo;
@@ -1653,7 +1066,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                 const uint64_t st_r1 = __builtin_amdgcn_s_memtime();
                 st_atom += st_r1 - st_r0;
 #endif
-#if SDK_PLANE_PRECONV
                 if (kk) {
 #if SDK_PLANE_STAMPS
                     const uint64_t st_r2 = __builtin_amdgcn_s_memtime();
@@ -1701,102 +1113,17 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     st_dep += __builtin_amdgcn_s_memtime() - st_r2;
 #endif
                 }
-#else
-                if (kk) {
-                    const uint32_t sh = plane_stage_span(io.seg_in((int64_t)base), io.seg_n((int64_t)base),
-                                                         io.seg_local((int64_t)base), kk, stage, lane);
-#if SDK_PLANE_STAMPS
-                    const uint64_t st_r2 = __builtin_amdgcn_s_memtime();
-                    st_dma += st_r2 - st_r1;
-#endif
-                    const int c1x = plane_slot_cell(lane & 31, 1);  // band 2, both halves
-                    uint32_t ad0 = c0 >= 0 ? sh + (uint32_t)c0 : (uint32_t)PLANE_STAGE_ZERO;
-                    uint32_t ad1 = c1x >= 0 ? sh + (uint32_t)c1x : (uint32_t)PLANE_STAGE_ZERO;
-                    const uint32_t st0 = c0 >= 0 ? 81u : 0u, st1 = c1x >= 0 ? 81u : 0u;
-                    const uint32_t mlo = lane < 32 ? 1u : 2u, mhi = lane < 32 ? 4u : 8u;
-                    uint64_t mm = idle, loaded = 0, bad = 0;
-                    // software-pipelined: the next board's bytes are read
-                    // while this board's ballots run (reads past the span
-                    // stay inside the staging area and are never used)
-                    uint32_t a0 = stage_b[ad0], a1 = stage_b[ad1];
-                    for (int j = 0; j < kk; ++j) {
-                        const int i = __builtin_ctzll(mm);
-                        mm &= mm - 1;
-                        ad0 += st0;
-                        ad1 += st1;
-                        const uint32_t n0 = stage_b[ad0], n1 = stage_b[ad1];
-                        const uint64_t s0 = __builtin_amdgcn_ballot_w64((a0 & 1u) != 0u);
-                        const uint64_t s1 = __builtin_amdgcn_ballot_w64((a0 & 2u) != 0u);
-                        const uint64_t s2 = __builtin_amdgcn_ballot_w64((a0 & 4u) != 0u);
-                        const uint64_t s3 = __builtin_amdgcn_ballot_w64((a0 & 8u) != 0u);
-                        const uint64_t u01 = __builtin_amdgcn_ballot_w64((a1 & mlo) != 0u);
-                        const uint64_t u23 = __builtin_amdgcn_ballot_w64((a1 & mhi) != 0u);
-                        if (__builtin_amdgcn_ballot_w64(a0 > 9u || a1 > 9u)) bad |= 1ull << i;
-                        loaded |= 1ull << i;
-#define PLANE_DROP(d, b, w) B.P[d][b] = (uint32_t)llvm_writelane((int)(uint32_t)(w), i, (int)B.P[d][b])
-                        PLANE_DROP(0, 0, s0); PLANE_DROP(0, 1, s0 >> 32); PLANE_DROP(0, 2, u01);
-                        PLANE_DROP(1, 0, s1); PLANE_DROP(1, 1, s1 >> 32); PLANE_DROP(1, 2, u01 >> 32);
-                        PLANE_DROP(2, 0, s2); PLANE_DROP(2, 1, s2 >> 32); PLANE_DROP(2, 2, u23);
-                        PLANE_DROP(3, 0, s3); PLANE_DROP(3, 1, s3 >> 32); PLANE_DROP(3, 2, u23 >> 32);
-#undef PLANE_DROP
-                        // the next board's bytes are consumed here, after this
-                        // board's ballots: their LDS latency is hidden
-                        asm volatile("" ::"v"(n0), "v"(n1));
-                        a0 = n0;
-                        a1 = n1;
-                    }
-                    if ((loaded >> lane) & 1u) {
-                        p = io.id((int64_t)base) + (int64_t)lanes_below(loaded);
-                        depth = 0;
-                        bguess = 0;
-                        mst = 0;
-                        if (!((bad >> lane) & 1u) &&
-                            !(best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p)) {
-                            uint32_t V[4][3], given[3];
-#pragma unroll
-                            for (int v = 0; v < 4; ++v)
-#pragma unroll
-                                for (int b = 0; b < 3; ++b) V[v][b] = B.P[v][b];
-                            plane::planes_from_slices(B, V, given);
-                            state = PL_ACTIVE;
-                        } else if (!((bad >> lane) & 1u)) {
-                            state = PL_CANCELLED;  // ordered mode: a lower board is solved
-                        }
-                    }
-                    // boards with a byte > 9 (or cancelled): the raw input back
-                    uint64_t r = loaded & __builtin_amdgcn_ballot_w64(state != PL_ACTIVE);
-                    while (r) {
-                        const int i = __builtin_ctzll(r);
-                        r &= r - 1;
-                        const int64_t q = io.id((int64_t)base) + (int64_t)__builtin_popcountll(loaded & ((1ull << i) - 1));
-                        plane_copy_board(io.src(q), io.dst(q), lane);
-                        if (lane == 0) {
-                            *io.stat(q) = ((bad >> i) & 1u) ? SDK_INVALID : SDK_CANCELLED;
-                            fin++;
-                        }
-                    }
-                    if (state == PL_CANCELLED) state = PL_IDLE;
-#if SDK_PLANE_STAMPS
-                    st_dep += __builtin_amdgcn_s_memtime() - st_r2;
-#endif
-                }
-#endif  // SDK_PLANE_PRECONV
             }
             // ---- tail: the queue is empty and the wave is down to a few
             // boards.  A pass costs the whole wave whatever its active
             // lanes, so the wave would idle on its slowest board for tens of
-            // passes; instead it hands them, one at a time, to the wave-wide
-            // solver (plane_wide.h: the search continues, ~150 instructions
-            // per pass) -- or, tail_mode 0, restarts each of them on the
-            // wave-per-board solver (packed_solver.h) -- and exits.
+            // passes; instead it hands them to the wave-wide solver
+            // (plane_wide.h: the search continues, ~200 instructions per
+            // pass) -- through its XCD's pool (tail mode 2), or one after
+            // the other itself (1) -- and exits.
             if (drained && tail > 0) {
                 const uint64_t act = __builtin_amdgcn_ballot_w64(state == PL_ACTIVE);
-                // policy 4: while waves of the XCD wait in the pool, hand over
-                // as many boards as the tail records hold (looked at every 8th time)
-                const bool steal = steal_on && act && __builtin_popcountll(act) <= PLANE_TAIL_MAX &&
-                                   (++steal_chk & 7u) == 0u && pool_load(steal_pool.word(POOL_HUNGRY)) > 0;
-                if (act && (__builtin_popcountll(act) <= tail || steal)) {
-                    if (state == PL_ACTIVE && !tail_mode) guesses -= bguess;  // those searches start over
+                if (act && __builtin_popcountll(act) <= tail) {
                     tail_act = act;
                     break;
                 }
@@ -1816,13 +1143,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         st_piters++;
 #endif
         uint32_t und[3];
-#if SDK_PLANE_ROWS_PERIOD
-        // rule D's box -> row form on every SDK_PLANE_ROWS_PERIOD-th
-        // iteration of the wave (a wave-uniform choice: one pass body runs)
-        const int r = plane::pass(B, und, rows_ctr == 0);
-#else
         const int r = plane::pass(B, und);
-#endif
         if (r == plane::STUCK && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < p) {
             state = PL_CANCELLED;  // ordered mode: a lower board is solved
             continue;
@@ -1855,7 +1176,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         }
     }
     if (ob_count) plane_flush_outbox(outbox, ob_count, lane, io);
-    if (steal_on) pool_add(steal_pool.word(POOL_LANE_LIVE), -1);
 #if SDK_PLANE_STAMPS
     const uint64_t st_tt = __builtin_amdgcn_s_memtime();
     const uint64_t st_t3 = __builtin_amdgcn_s_memrealtime();  // the lane loop ended
@@ -1867,8 +1187,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     const PlanePool pool = plane_pool(defer_list);
     // this launch's generation (arm_kernel, an earlier launch on the stream)
     const uint32_t gen = tail_mode >= 2 ? __builtin_amdgcn_readfirstlane((uint32_t)ws[WS_GEN]) : 0u;
-    uint64_t donated = 0;  // lanes whose stacks their pool records took along (other waves may use them)
-    if (tail_act && tail_mode) {
+    if (tail_act) {
         // ---- wave-wide tail: the lanes' boards go to LDS records (27 plane
         // words, index, depth, stack line, guesses; stride 33 dwords, so the
         // lanes' writes and a record's reads are conflict-free) and the wave
@@ -1880,7 +1199,6 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         if (tail_mode >= 2) {
             slot0 = (uint32_t)pool_add(pool.word(POOL_RESERVED), (int32_t)k);
             fit = slot0 >= PLANE_POOL_CAP ? 0u : (PLANE_POOL_CAP - slot0 < k ? PLANE_POOL_CAP - slot0 : k);
-            donated = __builtin_amdgcn_ballot_w64(((tail_act >> lane) & 1u) && rank < fit);
         }
         if ((tail_act >> lane) & 1u) {
             uint32_t v[PLANE_POOL_REC];
@@ -1920,27 +1238,10 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
             fin += wst[4];
             deferred += wst[3];
         }
-    } else if (tail_act) {
-        // after the loop: the planes are dead, the wave solver gets the registers
-        uint32_t wst[3];
-        plane_tail(tail_lds[threadIdx.x >> 6], lane, tail_act, (uint32_t)p, (uint32_t)(p >> 32), io, ws, best, order,
-                   wst);
-        if (lane == 0) {
-            solved += wst[0];
-            guesses += wst[1];
-            passes += wst[2];
-            fin += (uint32_t)__builtin_popcountll(tail_act);  // answered by the wave-per-board solver
-        }
     }
     if (tail_mode >= 2) {
         uint32_t wst[5] = {0u, 0u, 0u, 0u, 0u};
-        // a stack of this wave's that no pool record took along (tail <= 40 < 64 lanes)
-        const uint32_t own_off = (uint32_t)(g - lane + __builtin_ctzll(~donated)) * (uint32_t)(PLANE_MAX_DEPTH * 128);
-        if (tail_mode == 3)
-            plane_quad_drain(pool, lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after, gen, pool_polls, wst);
-        else
-            plane_pool_drain(pool, stage, lane, stk.rsrc, own_off, io, ws, defer_list, best, node_order, mrv_after,
-                             gen, pool_polls, split, wst);
+        plane_pool_drain(pool, lane, stk.rsrc, io, ws, defer_list, best, node_order, mrv_after, gen, pool_polls, wst);
         if (lane == 0) {
             solved += wst[0];
             guesses += wst[1];
@@ -1963,7 +1264,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
         if (lane == 6) st[6] = (int64_t)st_tail;
         if (lane == 7) st[7] = (int64_t)st_iters;
         if (lane == 8) st[8] = (int64_t)st_atom;
-        if (lane == 9) st[9] = (int64_t)st_dma;
+        if (lane == 9) st[9] = 0;
         if (lane == 10) st[10] = (int64_t)st_dep;
         if (lane == 11) st[11] = (int64_t)st_store;
         if (lane == 12) st[12] = (int64_t)st_t3;
@@ -1997,20 +1298,20 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel(
     const uint8_t *__restrict__ puzzles, uint8_t *__restrict__ sols, int32_t *__restrict__ status, int64_t n,
     unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack, int64_t *__restrict__ defer_list, int ordered,
-    int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after, uint32_t pool_polls, int split)
+    int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after, uint32_t pool_polls)
 {
     const PlaneIO1 io = {puzzles, sols, status, n};
-    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls, split);
+    plane_body(io, ws, stack, defer_list, ordered, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls);
 }
 
 // several batches, one queue over them (sdk_solve_batches; unordered)
 __global__ __launch_bounds__(PLANE_THREADS, SDK_PLANE_WAVES_PER_EU) void plane_kernel_multi(
     const PlaneBatches bs, unsigned long long *__restrict__ ws, uint32_t *__restrict__ stack,
     int64_t *__restrict__ defer_list, int order, int refill, int tail, int tail_mode, int chunk, uint32_t mrv_after,
-    uint32_t pool_polls, int split)
+    uint32_t pool_polls)
 {
     const PlaneIOn io = {bs};
-    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls, split);
+    plane_body(io, ws, stack, defer_list, 0, order, refill, tail, tail_mode, chunk, mrv_after, pool_polls);
 }
 
 #endif  // SDK_PLANE_KERNEL_H

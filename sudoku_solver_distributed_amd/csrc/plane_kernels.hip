@@ -14,8 +14,8 @@
 // runtime tuning knobs (A/B without a rebuild): $SDK_PLANE_REFILL idle lanes
 // before a wave refills, $SDK_PLANE_TAIL active lanes at or below which a
 // drained wave hands its last boards to the tail solver (0: off; at most
-// PLANE_TAIL_MAX), $SDK_PLANE_TAIL_MODE that solver (1: the wave-wide solver
-// continues each search, 0: the wave-per-board solver restarts it),
+// PLANE_TAIL_MAX), $SDK_PLANE_TAIL_MODE where the wave-wide solver continues
+// them (2: through the XCD's tail pool, 1: on the wave itself),
 // $SDK_PLANE_CHUNK most boards a wave claims from the queue at once (0: one
 // claim per refill), $SDK_PLANE_MRV passes on a board before its search
 // switches to the completion count (plane::search_step; 0: never).
@@ -37,7 +37,9 @@ static std::atomic<int> g_refill{-1}, g_tail{-1}, g_tail_mode{-1}, g_chunk{-1}, 
 
 int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 {
-    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode > 3 || refill == 0 || chunk > PLANE_CHUNK_MAX) return -1;
+    if (refill > 64 || tail > PLANE_TAIL_MAX || tail_mode == 0 || tail_mode > 2 || refill == 0 ||
+        chunk > PLANE_CHUNK_MAX)
+        return -1;
     if (refill < 0 && tail < 0 && tail_mode < 0 && chunk < 0) {
         g_refill = g_tail = g_tail_mode = g_chunk = -1;
         return 0;
@@ -52,7 +54,6 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk)
 struct PlaneKnobs {
     int refill, tail, tail_mode, chunk;
     uint32_t mrv_after, pool_polls;
-    int split;
 };
 
 static PlaneKnobs plane_knobs(int pipelined)
@@ -68,7 +69,7 @@ static PlaneKnobs plane_knobs(int pipelined)
     int tail = g_tail >= 0 ? g_tail.load() : pipelined ? pipe_tail_env : tail_env;
     tail = tail > PLANE_TAIL_MAX ? PLANE_TAIL_MAX : tail;
     int tail_mode = g_tail_mode >= 0 ? g_tail_mode.load() : pipelined ? pipe_tail_mode_env : tail_mode_env;
-    tail_mode = tail_mode < 0 ? 0 : tail_mode > 3 ? 3 : tail_mode;  // ($SDK_PLANE_*TAIL_MODE is not range-checked)
+    tail_mode = tail_mode < 1 ? 1 : tail_mode > 2 ? 2 : tail_mode;  // ($SDK_PLANE_*TAIL_MODE is not range-checked)
     int chunk = g_chunk >= 0 ? g_chunk.load() : chunk_env;
     chunk = chunk > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : chunk;  // ($SDK_PLANE_CHUNK is not range-checked)
     int mrv = g_mrv >= 0 ? g_mrv.load() : mrv_env;
@@ -77,11 +78,7 @@ static PlaneKnobs plane_knobs(int pipelined)
     // tests/test_gpu_full_size.py forces 0 to see the host raise, then
     // recovers on the same workspace)
     const uint32_t polls = (uint32_t)env_int("SDK_PLANE_POOL_POLLS", 1 << 23);
-    // split counting in the tail pool (plane_kernel.h): 0 off, 1 while waves
-    // wait for work, 2 at every chance (tests); read at every launch
-    int split = env_int("SDK_PLANE_SPLIT", SDK_PLANE_SPLIT);
-    split = split < 0 ? 0 : split > 4 ? 4 : split;
-    return {refill, tail, tail_mode, chunk, (uint32_t)mrv, polls, split};
+    return {refill, tail, tail_mode, chunk, (uint32_t)mrv, polls};
 }
 
 int sdk_set_plane_search(int mrv_after)
@@ -99,7 +96,7 @@ hipError_t sdk_launch_plane(const uint8_t *puzzles, uint8_t *sols, int32_t *stat
     const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, puzzles, sols, status, n, ws,
-                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls, k.split);
+                       stack, defer_list, ordered, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls);
     return hipGetLastError();
 }
 
@@ -109,7 +106,7 @@ hipError_t sdk_launch_plane_multi(const PlaneBatches &bs, unsigned long long *ws
     const PlaneKnobs k = plane_knobs(pipelined);
     const int64_t blocks = (threads + PLANE_THREADS - 1) / PLANE_THREADS;
     hipLaunchKernelGGL(plane_kernel_multi, dim3((unsigned)blocks), dim3(PLANE_THREADS), 0, st, bs, ws, stack,
-                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls, k.split);
+                       defer_list, order, k.refill, k.tail, k.tail_mode, k.chunk, k.mrv_after, k.pool_polls);
     return hipGetLastError();
 }
 

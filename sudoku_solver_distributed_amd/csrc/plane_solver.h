@@ -64,16 +64,24 @@
 #define SDK_PLANE_PIN_ACC 1
 #endif
 // pass() rule D (locked candidates), flags: 1 box -> column, 2 box -> row,
-// 4 column -> box; 0 off (only 1 pays on every pass: DESIGN.md §4).  The
-// box -> row form can also run on every SDK_PLANE_ROWS_PERIOD-th pass of the
-// plane kernel's lane loop only (pass()'s point_rows_on; plane_kernel.h)
+// 4 column -> box; 0 off (only 1 pays on every pass: DESIGN.md §4)
 #ifndef SDK_PLANE_LC
 #define SDK_PLANE_LC 1
 #endif
-// the same flags for the wave-wide and four-board tail solvers (plane_wide.h,
-// plane_quad.h), whose passes are latency- rather than issue-bound
+// the same flags for the wave-wide tail solver (plane_wide.h), whose passes
+// are latency- rather than issue-bound
 #ifndef SDK_WIDE_LC
 #define SDK_WIDE_LC SDK_PLANE_LC
+#endif
+// pass() rule C's hidden singles, applied in groups of SDK_PLANE_GROUP
+// digits: a digit's plane drops the singles of the EARLIER groups' digits
+// before its rules run, and those of its own group's lower digits after
+// them.  1 is Gauss-Seidel (one dependency chain through all nine digits);
+// with larger groups a group's rule chains are independent of each other
+// and the board is pinned once per group, so the group's chains interleave.
+// Every grouping is sound and reaches the same fixpoints.
+#ifndef SDK_PLANE_GROUP
+#define SDK_PLANE_GROUP 1
 #endif
 
 namespace plane {
@@ -180,9 +188,7 @@ PS_FN void pin_board(Board &B);
 // with literal constants, three-input logic as v_bitop3_b32 on VGPRs, right
 // shifts only, and one v_mul_u32_u24 per spread of a 9-bit set over three
 // rows.  ~1380 issue slots per pass (profiles/isa_plane_pass.json).
-// point_rows_on: rule D's box -> row form this pass (wave-uniform on the
-// GPU: one scalar branch after the digit loop)
-PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2) != 0)
+PS_FN int pass(Board &B, uint32_t und[3])
 {
     uint32_t single[3], nd[3];
     uint32_t dead = 0;
@@ -214,7 +220,7 @@ PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2
     const bool any_nd = or3(nd[0], nd[1], nd[2]) != 0;
     pin_board(B);
 
-    uint32_t hall[3] = {0u, 0u, 0u};
+    uint32_t hall[3] = {0u, 0u, 0u}, hgrp[3] = {0u, 0u, 0u};
     // per unit kind, "d has a place": row guard bits, columns, box bits 0/3/6
     uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
 #pragma unroll
@@ -225,7 +231,7 @@ PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2
         uint32_t x[3], f[3];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
-            if (d > 0) B.P[d][b] = andn(B.P[d][b], hall[b]);
+            if (d >= SDK_PLANE_GROUP) B.P[d][b] = andn(B.P[d][b], hgrp[b]);
             x[b] = nd[b] & B.P[d][b];
             f[b] = or3(x[b], x[b] >> 10, x[b] >> 20);  // bits 0-8: columns holding x (above: junk)
         }
@@ -305,8 +311,22 @@ PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2
         }
 #endif
 #pragma unroll
-        for (int b = 0; b < 3; ++b)
-            hall[b] = or_and(hall[b], B.P[d][b], bop3_nor(gr[b], hb[b], hcol));
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t hs = bop3_nor(gr[b], hb[b], hcol);  // d's single places (where d is possible)
+#if SDK_PLANE_GROUP > 1
+            if (d % SDK_PLANE_GROUP) {
+                // the singles of this group's lower digits leave d's plane, d's own stay
+                const uint32_t p = B.P[d][b];
+                B.P[d][b] = PS_BOP3(0xB0, p, hall[b], hs, p & ~(hall[b] & ~hs));
+                hall[b] = or_and(hall[b], p, hs);
+                continue;
+            }
+#endif
+            hall[b] = or_and(hall[b], B.P[d][b], hs);
+        }
+        if (d % SDK_PLANE_GROUP != SDK_PLANE_GROUP - 1 && d != 8) continue;
+#pragma unroll
+        for (int b = 0; b < 3; ++b) hgrp[b] = hall[b];  // what the next group's digits drop first
         pin_board(B);
         // the unit accumulators too: unpinned, the AND / OR chains over the
         // nine digits are re-associated into trees at the end of the pass,
@@ -335,8 +355,8 @@ PS_FN int pass(Board &B, uint32_t und[3], bool point_rows_on = (SDK_PLANE_LC & 2
             if (e) later |= B.P[e][b];
         }
     }
-#if SDK_PLANE_LC
-    if (point_rows_on) {
+#if SDK_PLANE_LC & 2
+    {
         // rule D's box -> row form, after the digit loop (its registers are
         // free again): every plane word once
 #pragma unroll

@@ -355,44 +355,23 @@ WD_FN void set_cell(V &w, const Lanes &L, int band, int pos, uint32_t dbit)
     w = pick(clr, andn(w, V(1u << pos)), w);
 }
 
-enum { W_UNSOLVABLE = 0, W_SOLVED = 1, W_OVERFLOW = -1, W_CANCELLED = 2, W_SUBTREE = 3 };
+enum { W_UNSOLVABLE = 0, W_SOLVED = 1, W_OVERFLOW = -1, W_CANCELLED = 2 };
 
 struct Stats {
     uint32_t passes, guesses, bguess;  // bguess: this board's guesses (lane + wide)
 };
 
-// ---- the search's hooks (the caller's policy)
-// cancelled(): ordered mode, a lower board has a completion.
-// counting(on): the board enters / leaves the completion count (M_COUNT).
-// Split counting (plane_kernel's tail pool): in M_COUNT the
-// order of subtrees does not matter, so untried digits of a board's stack
-// levels can be dealt out as separate searches.  try_split(w, depth, mst, stk,
-// L) may do that (and from then on split() is true); a split board's
-// completions and its subtrees' ends go through the board's shared
-// descriptor: completion(w) records one (false: it is the board's second --
-// this subtree stops, the walk decides, from the root), abandoned() tells a
-// subtree to stop (a second completion elsewhere), need_walk() records a
-// count too deep for the stack.  The walk's modes (M_WALK, M_FINAL) never
-// split: their order is the answer.
-struct NoSplit {
+// the search's hook: cancelled() -- ordered mode, a lower board has a completion
+struct NoCancel {
     WD_MF bool cancelled() const { return false; }
-    WD_MF void counting(bool) {}
-    WD_MF bool split() const { return false; }
-    template <class Stack>
-    WD_MF void try_split(const V &, uint32_t, uint32_t &, const Stack &, const Lanes &) {}
-    WD_MF bool completion(const V &) { return true; }
-    WD_MF bool abandoned() { return false; }
-    WD_MF void need_walk() {}
 };
 
 // Continue the search of the board in w at `depth` (levels below it on the
 // stack) to its first completion in walk order.  Stack: push(level, w, L,
 // entry), entry(level), restore(level, L), put_entry(level, e) over the
-// plane_kernel stack line layout.  hk: the hooks above.  mst / mrv_after:
+// plane_kernel stack line layout.  hk: the hook above.  mst / mrv_after:
 // the board's search mode, as the lane solver's (plane::search_step, the
-// same transitions).  Returns W_*; on W_SOLVED w holds the completion;
-// W_SUBTREE: a split board's share of the count is done (its descriptor
-// holds the outcome).
+// same transitions).  Returns W_*; on W_SOLVED w holds the completion.
 template <class Stack, class Hook>
 WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int node_order, uint32_t max_depth,
                 Stats &st, Hook &hk, uint32_t &mst, uint32_t mrv_after)
@@ -408,28 +387,22 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
         if (r == STUCK && plane::root_counts(mode, depth, mrv_after, rdl(und, 0), rdl(und, 16), rdl(und, 32))) {
             mode = plane::M_COUNT;  // a wide-open root: count at once (plane::search_step)
             mst = plane::mst_set_mode(mst, plane::M_COUNT);
-            hk.counting(true);
         }
         if (mode == plane::M_WALK && mrv_after && r != SOLVED && (mst & plane::MST_PASSES) >= mrv_after) {
             if (depth) w = stk.restore(0, L);  // the propagated root
             det = V(0u);
             depth = 0;
             mst = plane::mst_set_mode(mst, plane::M_COUNT);
-            hk.counting(true);
             continue;
         }
         if (r == OPEN) continue;
         if (r == SOLVED) {
             if (mode != plane::M_COUNT) return W_SOLVED;
-            if (hk.split()) {
-                if (!hk.completion(w)) return W_SUBTREE;  // the board's second: the walk decides
-                r = DEAD;                                 // the first: count on
-            } else if (mst & plane::MST_FOUND) {  // a second completion: the walk, from the root
+            if (mst & plane::MST_FOUND) {  // a second completion: the walk, from the root
                 w = stk.restore(0, L);
                 det = V(0u);
                 depth = 0;
                 mst = plane::mst_set_mode(mst, plane::M_FINAL);
-                hk.counting(false);
                 continue;
             } else {
                 mst |= plane::MST_FOUND;
@@ -440,22 +413,13 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
         if (r == STUCK) {
             if (depth == (mode == plane::M_COUNT ? sol_level : max_depth)) {
                 if (mode != plane::M_COUNT) return W_OVERFLOW;
-                if (hk.split()) {  // too deep to count: the walk decides, from the root
-                    hk.need_walk();
-                    return W_SUBTREE;
-                }
-                w = stk.restore(0, L);
+                w = stk.restore(0, L);  // too deep to count: the walk, from the root
                 det = V(0u);
                 depth = 0;
                 mst = plane::mst_set_mode(mst, plane::M_FINAL);
-                hk.counting(false);
                 continue;
             }
             if (hk.cancelled()) return W_CANCELLED;
-            if (mode == plane::M_COUNT) {
-                if (hk.split() && hk.abandoned()) return W_SUBTREE;
-                hk.try_split(w, depth, mst, stk, L);
-            }
             const uint32_t u[3] = {rdl(und, 0), rdl(und, 16), rdl(und, 32)};
             int band, pos;
             if (mode == plane::M_COUNT) {
@@ -481,7 +445,6 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
         // DEAD: back to the deepest level with an untried digit
         for (;;) {
             if (depth == 0) {
-                if (hk.split()) return W_SUBTREE;  // this share of the count is exhausted
                 if (mode == plane::M_COUNT && (mst & plane::MST_FOUND)) {  // exactly one completion
                     w = stk.restore(sol_level, L);
                     return W_SOLVED;

@@ -48,8 +48,8 @@ __global__ void arm_kernel(unsigned long long *ws, uint32_t *pool)
 {
     static_assert(PLANE_POOL_XCDS * PLANE_POOL_ARM_WORDS <= 64, "arm_kernel: one thread per pool word");
     if (pool && threadIdx.x < PLANE_POOL_XCDS * PLANE_POOL_ARM_WORDS) {
-        const uint32_t k = threadIdx.x % PLANE_POOL_ARM_WORDS;  // words 0..3 and 32..35 (plane_kernel.h POOL_*)
-        pool[(threadIdx.x / PLANE_POOL_ARM_WORDS) * PLANE_POOL_STRIDE + (k < 4 ? k : 28 + k)] = 0u;
+        const uint32_t k = threadIdx.x % PLANE_POOL_ARM_WORDS;  // the control words (plane_kernel.h POOL_*)
+        pool[(threadIdx.x / PLANE_POOL_ARM_WORDS) * PLANE_POOL_STRIDE + k] = 0u;
     }
     if (threadIdx.x == WS_QUEUE) ws[WS_QUEUE] = 0ull;
     if (threadIdx.x == WS_BEST) ws[WS_BEST] = (unsigned long long)INT64_MAX;
@@ -824,8 +824,6 @@ int sdk_read_stats(void *d_workspace, int64_t out[6], int reset, void *stream)
         // only sdk_verify_workspace clears it, once it has reported it)
         static_assert(WS_ASSIGNED == WS_FINISHED + 5, "counter words");
         e = hipMemsetAsync((unsigned long long *)d_workspace + WS_FINISHED, 0, 6 * sizeof(unsigned long long), st);
-        if (e == hipSuccess)
-            e = hipMemsetAsync((unsigned long long *)d_workspace + WS_SPLITS, 0, sizeof(unsigned long long), st);
         if (e == hipSuccess) e = hipStreamSynchronize(st);
         if (e != hipSuccess) return set_err("sdk_read_stats: reset", e);
     }
@@ -847,16 +845,14 @@ int sdk_verify_workspace(void *d_workspace, int64_t out[4], void *stream)
         out[0] = (int64_t)h[WS_ASSIGNED];
         out[1] = (int64_t)h[WS_FINISHED];
         out[2] = (int64_t)h[WS_ERROR];
-        out[3] = (int64_t)h[WS_SPLITS];
+        out[3] = 0;  // reserved
     }
     if (h[WS_ASSIGNED] == h[WS_FINISHED] && h[WS_ERROR] == 0) return 0;
     snprintf(g_err, sizeof g_err,
              "sdk_verify_workspace: %lld boards handed to the solve kernels, %lld answered; error bits 0x%llx%s "
              "(pool slot %llu)",
              (long long)h[WS_ASSIGNED], (long long)h[WS_FINISHED], h[WS_ERROR],
-             (h[WS_ERROR] & SDK_ERR_POOL_WAIT)   ? ": a tail-pool record was never published"
-             : (h[WS_ERROR] & SDK_ERR_POOL_IDLE) ? ": tail-pool waves waited on a count that never ended"
-                                                 : "",
+             (h[WS_ERROR] & SDK_ERR_POOL_WAIT) ? ": a tail-pool record was never published" : "",
              h[WS_ERR_SLOT]);
     // reported once: the next check starts from a consistent workspace
     unsigned long long fix[2] = {h[WS_FINISHED], 0ull};

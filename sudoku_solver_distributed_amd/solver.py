@@ -462,11 +462,11 @@ class BatchSolver:
         if rc == -3:
             raise SudokuHipError(self.lib.sdk_last_error().decode(errors="replace"))
         _lib.check(rc, "sdk_verify_workspace")
-        return {"assigned": out[0], "finished": out[1], "error": out[2], "splits": out[3]}
+        return {"assigned": out[0], "finished": out[1], "error": out[2]}
 
     def verify_inflight(self) -> dict:
         """verify() over the solve_inflight slots' workspaces (summed)."""
-        tot = {"assigned": 0, "finished": 0, "error": 0, "splits": 0}
+        tot = {"assigned": 0, "finished": 0, "error": 0}
         for solver, s in (self._slots or [(self, None)]):
             for k, v in solver.verify(stream=s).items():
                 tot[k] += v

@@ -148,11 +148,11 @@ static int pass(Board &B, uint32_t und[3])
     }
     const bool all_single = (single[0] & single[1] & single[2]) == ROWS;
     const bool any_nd = (nd[0] | nd[1] | nd[2]) != 0;
-    uint32_t hall[3] = {0u, 0u, 0u};
+    uint32_t hall[3] = {0u, 0u, 0u}, hgrp[3] = {0u, 0u, 0u};
     uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
     for (int d = 0; d < 9; ++d) {
-        if (d > 0)
-            for (int b = 0; b < 3; ++b) B.P[d][b] &= ~hall[b];
+        if (d >= SDK_PLANE_GROUP)  // the singles of the earlier groups' digits
+            for (int b = 0; b < 3; ++b) B.P[d][b] &= ~hgrp[b];
         uint32_t x[3], f[3];
         for (int b = 0; b < 3; ++b) {
             x[b] = nd[b] & B.P[d][b];
@@ -222,7 +222,13 @@ static int pass(Board &B, uint32_t und[3])
             B.P[d][b] &= ~m;
         }
 #endif
-        for (int b = 0; b < 3; ++b) hall[b] |= (hb[b] | hcol) & B.P[d][b];  // (after rule D)
+        for (int b = 0; b < 3; ++b) {
+            const uint32_t hd = (hb[b] | hcol) & B.P[d][b];  // (after rule D)
+            B.P[d][b] = (B.P[d][b] & ~hall[b]) | hd;  // this group's lower digits' singles leave, d's own stay
+            hall[b] |= hd;
+        }
+        if (d % SDK_PLANE_GROUP == SDK_PLANE_GROUP - 1)
+            for (int b = 0; b < 3; ++b) hgrp[b] = hall[b];
     }
     for (int b = 0; b < 3; ++b) {
         uint32_t later = B.P[8][b];

@@ -6,10 +6,7 @@
 #include <stdint.h>
 #include <string.h>
 
-#include <deque>
-#include <vector>
 
-#include "../../sudoku_solver_distributed_amd/csrc/plane_quad.h"
 #include "../../sudoku_solver_distributed_amd/csrc/plane_wide.h"
 
 enum { LEVEL_WORDS = 32, MAX_LEVELS = 82 };
@@ -133,7 +130,7 @@ extern "C" void wide_solve_batch(const uint8_t *in, uint8_t *out, int32_t *statu
         // ---- wide phase: same planes (Det dropped), same stack and depth
         wide::V w = to_wave(B, L);
         wide::Stats st = {0, 0, 0};
-        wide::NoSplit hk;
+        wide::NoCancel hk;
         const int r = wide::solve(w, depth, stk, L, node_order, max_depth, st, hk, mst, g_mrv_after);
         g += st.guesses;
         pw += st.passes;
@@ -216,276 +213,6 @@ extern "C" int64_t wide_check_fixpoint(const uint8_t *in, int64_t n, int trials,
                     for (int k = 0; k < 64; ++k)
                         if ((L.valid.m >> k) & 1) E.P[L.d.x[k]][L.b.x[k]] = w.x[k];
                 bad += !determined_clash(E);
-            }
-        }
-    }
-    return bad;
-}
-
-// ---- split counting over an emulated tail pool (plane_kernel.h PoolHook /
-// plane_pool_drain, the same wide::solve hooks): every board is handed to
-// the pool after `lane_guesses` lane guesses; records are solved one at a
-// time in FIFO order (the boards' records interleave), and a count-mode
-// search deals the untried digits of its shallowest open level out as new
-// records whenever the pseudo-random "a wave is hungry" signal fires (every
-// chance with split_every 1).  The last subtree of a split board answers it:
-// no completion / the one / the walk from the count's root.  Answers must be
-// the lane solver's and the oracle's whatever the split schedule.
-struct Desc {
-    int out = 0, compl_ = 0;
-    bool walk = false;
-    int64_t board = 0;
-    wide::V found, root;
-};
-struct Rec {
-    wide::V w;
-    int64_t board;
-    uint32_t depth, mst, bguess;
-    int desc;                       // -1: a whole board
-    std::vector<uint32_t> stack;    // its stack levels (a whole board brings the lane's)
-};
-
-struct HostPool {
-    std::deque<Rec> q;
-    std::vector<Desc> descs;
-    uint32_t rs, every;
-    uint64_t splits = 0, records = 0;
-    bool hungry()
-    {
-        rs ^= rs << 13;
-        rs ^= rs >> 17;
-        rs ^= rs << 5;
-        return every <= 1 || rs % every == 0;
-    }
-};
-
-struct HostHook {
-    HostPool &pool;
-    int64_t board;
-    int desc;
-    uint32_t sol_level;
-    bool cancelled() const { return false; }
-    void counting(bool) {}
-    bool split() const { return desc >= 0; }
-    bool completion(const wide::V &w)
-    {
-        Desc &D = pool.descs[desc];
-        if (D.compl_++ == 0) D.found = w;
-        return D.compl_ == 1;
-    }
-    bool abandoned() { return pool.descs[desc].compl_ >= 2 || pool.descs[desc].walk; }
-    void need_walk() { pool.descs[desc].walk = true; }
-    template <class Stack>
-    void try_split(const wide::V &, uint32_t depth, uint32_t &mst, const Stack &stk, const wide::Lanes &L)
-    {
-        if (depth == 0 || !pool.hungry()) return;
-        uint32_t e = 0;
-        const uint64_t open = stk.open_levels(depth, e);
-        if (!open) return;
-        const uint32_t lvl = (uint32_t)__builtin_ctzll(open);
-        const uint32_t rem = (e >> 8) & 0x1FFu;
-        if (desc < 0) {
-            Desc D;
-            D.out = 1;
-            D.board = board;
-            D.root = stk.restore(0, L);
-            if (mst & plane::MST_FOUND) {
-                D.compl_ = 1;
-                D.found = stk.restore(sol_level, L);
-            }
-            mst &= ~plane::MST_FOUND;
-            pool.descs.push_back(D);
-            desc = (int)pool.descs.size() - 1;
-        }
-        pool.splits++;
-        const wide::V base = stk.restore(lvl, L);
-        uint32_t left = rem;
-        while (left) {
-            const uint32_t dbit = left & (0u - left);
-            left ^= dbit;
-            Rec r;
-            r.w = base;
-            wide::set_cell(r.w, L, (int)((e >> 5) & 3u), (int)(e & 31u), dbit);
-            r.board = board;
-            r.depth = 0;
-            r.mst = plane::mst_set_mode(0u, plane::M_COUNT);
-            r.bguess = 0;
-            r.desc = desc;
-            r.stack.assign(MAX_LEVELS * LEVEL_WORDS, 0u);
-            pool.q.push_back(std::move(r));
-            pool.descs[desc].out++;
-        }
-        stk.put_entry(lvl, e & ~(rem << 8));
-    }
-};
-
-// status: 1 solved, 0 no completion, -1 invalid byte, 2 left to the wave
-// kernel; splits: split events, records: records solved
-extern "C" void wide_split_solve_batch(const uint8_t *in, uint8_t *out, int32_t *status, int64_t n, int node_order,
-                                       uint32_t max_depth, uint32_t lane_guesses, uint32_t split_every, uint32_t seed,
-                                       uint64_t *splits, uint64_t *records)
-{
-    const wide::Lanes L = wide::lanes();
-    HostPool pool;
-    pool.rs = seed * 2654435761u + 1u;
-    pool.every = split_every;
-    for (int64_t i = 0; i < n; ++i) {
-        const uint8_t *src = in + i * 81;
-        uint8_t *dst = out + i * 81;
-        memcpy(dst, src, 81);
-        status[i] = 77;
-        uint32_t x[21];
-        words_of(src, x);
-        plane::Board B;
-        bool clash = false;
-        if (!plane::load_words(B, x, clash)) { status[i] = -1; continue; }
-        if (clash) { status[i] = 2; continue; }
-        uint32_t depth = 0, lg = 0, mst = 0;
-        int done = -2;
-        const plane::WordStack<LineStack> ls = {lines};
-        while (lg < lane_guesses) {
-            uint32_t und[3];
-            const int r = plane::pass(B, und);
-            const int s = plane::search_step(B, und, r, depth, mst, ls, node_order, max_depth, g_mrv_after, lg);
-            if (s == plane::S_CONT) continue;
-            done = s == plane::S_SOLVED ? 1 : s == plane::S_NONE ? 0 : -1;
-            break;
-        }
-        if (done == 1) {
-            plane::store_values(B, [&](int c, uint32_t v) { dst[c] = (uint8_t)v; });
-            status[i] = 1;
-            continue;
-        }
-        if (done == 0) { status[i] = 0; continue; }
-        if (done == -1) { status[i] = 2; continue; }
-        Rec r;
-        r.w = to_wave(B, L);
-        r.board = i;
-        r.depth = depth;
-        r.mst = mst;
-        r.bguess = lg;
-        r.desc = -1;
-        r.stack.assign(stack_words, stack_words + MAX_LEVELS * LEVEL_WORDS);  // the lane's stack goes along
-        pool.q.push_back(std::move(r));
-    }
-    auto answer = [&](int r, const wide::V &w, int64_t b) {
-        if (r == wide::W_SOLVED) {
-            store_wave(w, L, out + b * 81);
-            status[b] = 1;
-        } else {
-            status[b] = r == wide::W_UNSOLVABLE ? 0 : 2;
-        }
-    };
-    while (!pool.q.empty()) {
-        Rec rec = std::move(pool.q.front());
-        pool.q.pop_front();
-        pool.records++;
-        const WStack stk = {rec.stack.data()};
-        wide::Stats st = {0, 0, rec.bguess};
-        HostHook hk = {pool, rec.board, rec.desc, max_depth - 1};
-        wide::V w = rec.w;
-        uint32_t depth = rec.depth, mst = rec.mst;
-        int r = wide::solve(w, depth, stk, L, node_order, max_depth, st, hk, mst, g_mrv_after);
-        if (r != wide::W_SUBTREE) {
-            answer(r, w, rec.board);
-            continue;
-        }
-        Desc &D = pool.descs[hk.desc];
-        if (--D.out) continue;
-        if (D.compl_ >= 2 || D.walk) {  // the walk decides, from the count's root
-            std::vector<uint32_t> own(MAX_LEVELS * LEVEL_WORDS, 0u);
-            const WStack os = {own.data()};
-            wide::V fw = D.root;
-            uint32_t d0 = 0, m0 = plane::mst_set_mode(0u, plane::M_FINAL);
-            wide::Stats fs = {0, 0, 0};
-            wide::NoSplit nh;
-            answer(wide::solve(fw, d0, os, L, node_order, max_depth, fs, nh, m0, g_mrv_after), fw, D.board);
-        } else {
-            answer(D.compl_ == 1 ? wide::W_SOLVED : wide::W_UNSOLVABLE, D.found, D.board);
-        }
-    }
-    *splits = pool.splits;
-    *records = pool.records;
-}
-
-// ---- the four-board pass (plane_quad.h) against the lane pass: boards four
-// at a time (row q = board 4k+q), from each loaded board and from `trials`
-// random mid-search states, both passes iterated to their first non-OPEN
-// result per board.  Returns the states where verdict, planes or
-// undetermined cells differ, the same admitted exception as
-// wide_check_fixpoint (a duplicated determined digit neither flags at once).
-extern "C" int64_t quad_check_fixpoint(const uint8_t *in, int64_t n, int trials, uint32_t seed)
-{
-    const quad::Lanes QL = quad::lanes();
-    int64_t bad = 0;
-    uint32_t rs = seed * 2654435761u + 7u;
-    auto rnd = [&rs]() { rs ^= rs << 13; rs ^= rs >> 17; rs ^= rs << 5; return rs; };
-    for (int trial = 0; trial <= trials; ++trial) {
-        for (int64_t i0 = 0; i0 < n; i0 += 4) {
-            plane::Board B[4];
-            bool ok[4] = {false, false, false, false};
-            int rl[4] = {0, 0, 0, 0};
-            uint32_t ul[4][3] = {};
-            for (int q = 0; q < 4 && i0 + q < n; ++q) {
-                uint32_t x[21];
-                words_of(in + (i0 + q) * 81, x);
-                bool clash = false;
-                if (!plane::load_words(B[q], x, clash) || clash) continue;
-                const int guesses = trial ? 1 + (int)(rnd() % 4) : 0;
-                int r = plane::STUCK;
-                for (int k = 0; k < guesses; ++k) {
-                    while ((r = plane::pass(B[q], ul[q])) == plane::OPEN) {}
-                    if (r != plane::STUCK) break;
-                    int band, pos;
-                    plane::pick_cell(ul[q], (int)(rnd() & 1u), band, pos);
-                    uint32_t d = plane::cell_cand(B[q], band, pos);
-                    for (uint32_t j = rnd() % (uint32_t)__builtin_popcount(d); j; --j) d &= d - 1;
-                    plane::set_cell(B[q], band, pos, d & (0u - d));
-                }
-                ok[q] = r == plane::STUCK;
-            }
-            // the quad wave from the same states (Det carried over)
-            wide::V w[3], det[3], und[3];
-            for (int b = 0; b < 3; ++b) w[b] = det[b] = und[b] = wide::V(0u);
-            for (int k = 0; k < 64; ++k) {
-                const int q = k >> 4, d = k & 15;
-                if (!ok[q] || d >= 9) continue;
-                for (int b = 0; b < 3; ++b) {
-                    w[b].x[k] = B[q].P[d][b];
-                    det[b].x[k] = B[q].Det[b];
-                }
-            }
-            for (int q = 0; q < 4; ++q)
-                if (ok[q])
-                    while ((rl[q] = plane::pass(B[q], ul[q])) == plane::OPEN) {}
-            int rw[4] = {-1, -1, -1, -1};
-            for (int it = 0; it < 200; ++it) {
-                const wide::V r = quad::pass(w, det, und, QL);
-                bool more = false;
-                for (int q = 0; q < 4; ++q) {
-                    if (!ok[q] || rw[q] >= 0) continue;
-                    if (r.x[16 * q] != (uint32_t)quad::OPEN) rw[q] = (int)r.x[16 * q];
-                    else more = true;
-                    for (int k = 16 * q; k < 16 * q + 16; ++k)
-                        if (r.x[k] != r.x[16 * q]) bad += 1000000;  // not row-uniform
-                }
-                if (!more) break;  // (a row past its verdict: STUCK / SOLVED are fixpoints, DEAD is not compared)
-            }
-            for (int q = 0; q < 4; ++q) {
-                if (!ok[q]) continue;
-                bool diff = rl[q] != rw[q];
-                if (!diff && rl[q] == plane::STUCK) {
-                    for (int d = 0; d < 9; ++d)
-                        for (int b = 0; b < 3; ++b) diff |= w[b].x[16 * q + d] != B[q].P[d][b];
-                    for (int b = 0; b < 3; ++b) diff |= und[b].x[16 * q] != ul[q][b];
-                }
-                if (diff) {
-                    plane::Board E = B[q];
-                    if (rw[q] == quad::STUCK)
-                        for (int d = 0; d < 9; ++d)
-                            for (int b = 0; b < 3; ++b) E.P[d][b] = w[b].x[16 * q + d];
-                    bad += !determined_clash(E);
-                }
             }
         }
     }

@@ -95,10 +95,10 @@ def test_plane_tuning_arguments():
     assert f(65, -1, -1, -1) == -1      # refill > 64
     assert f(0, -1, -1, -1) == -1       # refill 0: a wave would never refill
     assert f(-1, 41, -1, -1) == -1      # tail > 40 (LDS records)
-    assert f(-1, -1, 4, -1) == -1       # tail mode 0 / 1 / 2 / 3 only
+    assert f(-1, -1, 3, -1) == -1       # tail mode 1 / 2 only
+    assert f(-1, -1, 0, -1) == -1
     assert f(-1, -1, 2, -1) == 0        # the per-XCD tail pool
-    assert f(-1, -1, 3, -1) == 0        # the same on the four-board solver
-    assert f(8, 40, 0, 32) == 0
+    assert f(8, 40, 1, 32) == 0
     assert f(-1, 0, -1, -1) == 0        # tail off
     assert f(-1, -1, -1, -1) == 0       # defaults back
 

@@ -1,8 +1,8 @@
 """Several batches per launch (sdk_solve_batches / BatchSolver.solve_batches,
 the strong-scaling steps): every batch's bytes and statuses equal what
 solve() gives it alone -- the queue runs over the batches laid end to end, so
-claims, static hand-out windows, staged spans, the outbox, the wave-wide and
-restart tails and the deferred list all cross batch boundaries here."""
+claims, static hand-out windows, staged spans, the outbox, the wave-wide
+tails, the XCD pool and the deferred list all cross batch boundaries here."""
 import numpy as np
 import pytest
 import torch
@@ -61,12 +61,12 @@ def test_solve_batches_sixteen_unaligned(solver):
     _check_same(solver, batches, "node", 2)
 
 
-def test_solve_batches_restart_tail(solver):
-    """The restart tail (tail_mode 0: a drained wave's last boards restarted
-    on the wave-per-board solver) and the widest tail, through several batches."""
+def test_solve_batches_widest_tail(solver):
+    """The widest tail (40 boards per wave, on the wave itself and through the
+    XCD pool) and one-board claims, through several batches."""
     lib = solver.lib
     try:
-        assert lib.sdk_set_plane_tuning(-1, 40, 0, -1) == 0
+        assert lib.sdk_set_plane_tuning(-1, 40, 2, -1) == 0
         _check_same(solver, _mixed(200), "gen", 1)
         assert lib.sdk_set_plane_tuning(-1, 40, 1, 1) == 0   # one-board claims
         _check_same(solver, _mixed(300), "node", 0)
@@ -150,7 +150,7 @@ def test_search_mode_switch_same_results(solver, order):
         assert np.array_equal(want[0][g0:g1].cpu().numpy(), w) and np.array_equal(want[1][g0:g1].cpu().numpy(), ws)
         for k in (1, 8, 48, 128):
             assert lib.sdk_set_plane_search(k) >= 0
-            for tail, mode in ((8, 1), (16, 2), (40, 2), (12, 3), (40, 3)):  # own tail / XCD pool / four-board pool
+            for tail, mode in ((8, 1), (16, 2), (40, 2)):  # own tail / XCD pool
                 assert lib.sdk_set_plane_tuning(-1, tail, mode, -1) == 0
                 got = solver.solve(p, order=order)
                 torch.cuda.synchronize()
@@ -204,79 +204,3 @@ def test_pipelined_flag_same_results(solver):
         assert torch.equal(torch.cat(outs), a[0]) and torch.equal(torch.cat(sts), a[1]), last
     with pytest.raises(ValueError):
         solver.solve(p[:10], grid_waves=1 << 16)
-
-
-def _nosol_boards(n, seed):
-    """Unique 17-clue boards with one wrong clue that repeats no given in its
-    units: no completion (the unique counter pins the walk's answer)."""
-    from sudoku_solver_distributed_amd.gen import hard17_batch
-    rng = np.random.default_rng(seed)
-    b = hard17_batch(n, seed=seed).numpy()
-    sols, _ = O.solve_unique_batch(b)
-    for i in range(n):
-        for c in rng.permutation(np.nonzero(b[i] == 0)[0]):
-            r, k = divmod(int(c), 9)
-            peers = set(b[i, r * 9:r * 9 + 9]) | set(b[i, k::9]) | {
-                b[i, (r // 3 * 3 + j // 3) * 9 + k // 3 * 3 + j % 3] for j in range(9)}
-            ok = [d for d in range(1, 10) if d not in peers and d != sols[i, c]]
-            if ok:
-                b[i, c] = ok[0]
-                break
-    return b
-
-
-@pytest.mark.parametrize("order", ["gen", "node"])
-def test_split_count_same_results(solver, order):
-    """Split counting in the tail pool (plane_kernel.h PoolHook): count-mode
-    boards deal the untried digits of their shallowest open stack level out
-    to other waves.  Bytes and statuses never depend on it -- off, while
-    waves wait (the default), at every chance -- on hard 17-clue boards, many
-    completions (the last subtree hands the board to the walk from the
-    count's root), none, search-heavy boards, invalid bytes and clashing
-    givens, with the search-mode switch at 1, 8 and 64 passes and the pool
-    taking 12 or 40 boards per wave; every board answered (verify), and the
-    forced policy really deals subtrees out."""
-    import os
-    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
-    lib = solver.lib
-    rng = np.random.default_rng(31)
-    grids, _ = O.solve_unique_batch(hard17_batch(2000, seed=32).numpy())
-    for g in grids:
-        g[rng.choice(81, 56, replace=False)] = 0
-    nosol = _nosol_boards(300, 33)
-    parts = [hard17_batch(30_000, seed=34), torch.from_numpy(grids), torch.from_numpy(nosol),
-             hard_search_batch(8000, seed=35)]
-    p = torch.cat(parts).cuda()
-    p[17, 3] = 11
-    p[35_000] = torch.tensor(b81(CLASH), dtype=torch.uint8)
-    try:
-        os.environ["SDK_PLANE_SPLIT"] = "0"
-        want = [t.clone() for t in solver.solve(p, order=order)]
-        torch.cuda.synchronize()
-        # oracle: the unique boards by the counter, the many-completion ones by the walk
-        wu, _ = O.solve_unique_batch(p[:30_000].cpu().numpy())
-        assert np.array_equal(want[0][:30_000].cpu().numpy(), wu)
-        wg, wgs = O.solve_batch(grids, order=order)
-        assert np.array_equal(want[0][30_000:32_000].cpu().numpy(), wg)
-        assert np.array_equal(want[1][30_000:32_000].cpu().numpy(), wgs)
-        assert bool((want[1][32_000:32_300] == 0).all())
-        assert torch.equal(want[0][32_000:32_300].cpu(), torch.from_numpy(nosol))
-        splits = 0
-        for split in ("1", "2"):
-            os.environ["SDK_PLANE_SPLIT"] = split
-            for mrv in (1, 8, 64):
-                assert lib.sdk_set_plane_search(mrv) >= 0
-                for tail in (12, 40):
-                    assert lib.sdk_set_plane_tuning(-1, tail, 2, -1) == 0
-                    solver.stats(reset=True)
-                    got = solver.solve(p, order=order)
-                    torch.cuda.synchronize()
-                    v = solver.verify()
-                    assert torch.equal(got[0], want[0]) and torch.equal(got[1], want[1]), (split, mrv, tail)
-                    assert v["finished"] == v["assigned"] == p.shape[0]
-                    splits += v["splits"] if split == "2" else 0
-        assert splits > 0
-    finally:
-        os.environ.pop("SDK_PLANE_SPLIT", None)
-        lib.sdk_set_plane_search(-1)
-        lib.sdk_set_plane_tuning(-1, -1, -1, -1)

@@ -431,13 +431,12 @@ def test_hard_search_4m(solver):
     assert np.array_equal(sols[idx.to(p.device)].cpu().numpy(), want)
 
 
-@pytest.mark.parametrize("tail,mode", [(40, 1), (40, 0), (0, 1), (40, 2), (8, 2), (40, 3), (12, 3)])
+@pytest.mark.parametrize("tail,mode", [(40, 1), (0, 1), (40, 2), (8, 2)])
 def test_plane_tail_paths(solver, tail, mode):
     """The plane kernel's drained-wave tail (sdk_set_plane_tuning): with 40
     the most boards of every wave end on the tail solver -- wave-wide
-    continuation (mode 1, plane_wide.h), through the XCD pool (2) or the
-    pool on the four-board solver (3, plane_quad.h), or wave-per-board
-    restart (mode 0); 0 switches the tail off.  Search-heavy and hard boards against their
+    continuation (mode 1, plane_wide.h) or through the XCD pool (2); 0
+    switches the tail off.  Search-heavy and hard boards against their
     unique completion, generated multi-solution boards against the literal
     walk in both orders, clashing givens (deferred from the tail), an empty
     board deeper than the stack (deferred), ordered mode."""

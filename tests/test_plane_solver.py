@@ -191,8 +191,6 @@ def wide(tmp_path_factory):
     lib.wide_check_fixpoint.restype = ctypes.c_int64
     lib.wide_set_mrv_after.argtypes = [ctypes.c_uint32]
     lib.wide_set_mrv_after(0)
-    lib.quad_check_fixpoint.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
-    lib.quad_check_fixpoint.restype = ctypes.c_int64
     return lib
 
 
@@ -227,17 +225,6 @@ def test_wide_fixpoint_matches_lane_pass(wide):
     a unit (wide_host.cpp wide_check_fixpoint)."""
     boards = _mixed_boards()
     assert wide.wide_check_fixpoint(boards.ctypes.data, len(boards), 20, 5) == 0
-
-
-def test_quad_fixpoint_matches_lane_pass(wide):
-    """The four-board pass (plane_quad.h: row q of the wave holds board q,
-    lane 16q+d digit d's three band words) reaches the lane pass's fixpoint
-    for every board of every row -- same verdict, planes and undetermined
-    cells, row-uniform results -- from each board and from 20 random
-    mid-search states, four different boards per emulated wave (the same
-    admitted exception as the wave-wide pass)."""
-    boards = _mixed_boards()
-    assert wide.quad_check_fixpoint(boards.ctypes.data, len(boards), 20, 7) == 0
 
 
 @pytest.mark.parametrize("order", ["gen", "node"])
@@ -287,82 +274,20 @@ def test_wide_edge_cases(wide):
 
 # ---- split counting over an emulated tail pool (plane_kernel.h PoolHook)
 
-def _split(lib, boards, node_order=0, lane_guesses=0, every=1, seed=1, max_depth=32):
-    vp = ctypes.c_void_p
-    lib.wide_split_solve_batch.argtypes = [vp, vp, vp, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32,
-                                           ctypes.c_uint32, ctypes.c_uint32, vp, vp]
-    boards = np.ascontiguousarray(boards, dtype=np.uint8).reshape(-1, 81)
-    out = np.zeros_like(boards)
-    st = np.zeros(len(boards), dtype=np.int32)
-    sp, rc = ctypes.c_uint64(), ctypes.c_uint64()
-    lib.wide_split_solve_batch(boards.ctypes.data, out.ctypes.data, st.ctypes.data, len(boards), node_order,
-                               max_depth, lane_guesses, every, seed, ctypes.byref(sp), ctypes.byref(rc))
-    return out, st, sp.value, rc.value
-
-
-@pytest.mark.parametrize("order", ["gen", "node"])
-@pytest.mark.parametrize("mrv", [1, 24])
-def test_split_count_vs_oracle(wide, order, mrv):
-    """Count-mode subtrees dealt out as pool records (split every chance,
-    every other, one in five), in FIFO order interleaved with other boards,
-    after 0 / 1 / 3 lane guesses: boards with one completion, many (the last
-    subtree sends the board to the walk from the count's root), none (a wrong
-    clue on a unique board) and search-heavy ones -- every answer and status
-    the oracle's walk, bit for bit."""
-    from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
-    rng = np.random.default_rng(5)
-    grids, _ = O.solve_unique_batch(hard17_batch(120, seed=9).numpy())
-    for g in grids:
-        g[rng.choice(81, 56, replace=False)] = 0          # many completions
-    nosol = hard17_batch(60, seed=10).numpy()
-    sols, _ = O.solve_unique_batch(nosol)
-    for i in range(60):  # no completion: a wrong clue that repeats no given in its units
-        b = nosol[i]
-        for c in rng.permutation(np.nonzero(b == 0)[0]):
-            r, k = divmod(int(c), 9)
-            peers = set(b[r * 9:r * 9 + 9]) | set(b[k::9]) | {b[(r // 3 * 3 + j // 3) * 9 + k // 3 * 3 + j % 3]
-                                                              for j in range(9)}
-            ok = [d for d in range(1, 10) if d not in peers and d != sols[i, c]]
-            if ok:
-                b[c] = ok[0]
-                break
-    boards = np.ascontiguousarray(np.concatenate([hard17_batch(150, seed=11).numpy(), grids, nosol,
-                                                  hard_search_batch(120, seed=12).numpy()]))
-    # one completion / none: the counter pins the walk's answer (the walk on a
-    # no-completion board can take astronomically long); many: the literal walk
-    wu, cnt = O.solve_unique_batch(boards[:150])
-    wg, wgs = O.solve_batch(boards[150:270], order=order)
-    wn, cn = O.solve_unique_batch(boards[270:330])
-    wh, ch = O.solve_unique_batch(boards[330:])
-    assert (cnt == 1).all() and (cn == 0).all() and (ch == 1).all()
-    want = np.concatenate([wu, wg, boards[270:330], wh])
-    wst = np.concatenate([np.ones(150, np.int32), wgs, np.zeros(60, np.int32), np.ones(120, np.int32)])
-    no = int(order == "node")
-    wide.wide_set_mrv_after(mrv)
-    try:
-        total = 0
-        for every, lg in ((1, 0), (2, 1), (5, 3)):
-            got, st, splits, recs = _split(wide, boards, no, lg, every, seed=every + 10 * lg)
-            assert np.array_equal(st, wst), (every, lg)
-            assert np.array_equal(got, want), (every, lg)
-            total += splits
-        assert total > 100  # the count was really dealt out
-    finally:
-        wide.wide_set_mrv_after(0)
-
-
-@pytest.mark.parametrize("flags", [0, 3, 5, 7])
-def test_rule_d_variants_match_their_restatement(tmp_path, flags):
+@pytest.mark.parametrize("flags,group", [(0, 1), (3, 1), (5, 1), (7, 1), (1, 2), (1, 3), (1, 9), (7, 2)])
+def test_pass_variants_match_their_restatement(tmp_path, flags, group):
     """Every SDK_PLANE_LC rule-D variant (0 none, 1 box -> column -- the
-    default, covered above --, 2 box -> row, 4 column -> box) keeps the
-    pass equal to its plain-loop restatement (plane_host.cpp v1::pass) after
-    every pass, and the wave-wide and four-board passes reach its fixpoints
-    (wide_host.cpp), so a build with other flags stays exact."""
-    define = "-DSDK_PLANE_LC=%d" % flags
+    default, covered above --, 2 box -> row, 4 column -> box) and every
+    SDK_PLANE_GROUP grouping of rule C's hidden singles (1 Gauss-Seidel, the
+    default; 2 and 3 digits per group; 9 Jacobi) keeps the pass equal to its
+    plain-loop restatement (plane_host.cpp v1::pass) after every pass, and
+    the wave-wide pass reaches its fixpoints (wide_host.cpp), so a build with
+    other flags stays exact."""
+    defines = ["-DSDK_PLANE_LC=%d" % flags, "-DSDK_PLANE_GROUP=%d" % group]
     libs = {}
     for name in ("plane_host", "wide_host"):
-        out = str(tmp_path / ("lib%s_%d.so" % (name, flags)))
-        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", define, "-o", out,
+        out = str(tmp_path / ("lib%s_%d_%d.so" % (name, flags, group)))
+        subprocess.check_call(["g++", "-O2", "-shared", "-fPIC", "-std=c++17", *defines, "-o", out,
                                os.path.join(NATIVE, name + ".cpp")])
         libs[name] = ctypes.CDLL(out)
     from sudoku_solver_distributed_amd.gen import hard17_batch, hard_search_batch
@@ -372,11 +297,19 @@ def test_rule_d_variants_match_their_restatement(tmp_path, flags):
     chk.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_uint64]
     chk.restype = ctypes.c_int64
     assert chk(boards.ctypes.data, len(boards), 50_000, 5) == 0
-    for fn in ("wide_check_fixpoint", "quad_check_fixpoint"):
-        f = getattr(libs["wide_host"], fn)
-        f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
-        f.restype = ctypes.c_int64
-        assert f(boards[:100].ctypes.data, 100, 5, 3) == 0, fn
+    f = libs["wide_host"].wide_check_fixpoint
+    f.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_uint32]
+    f.restype = ctypes.c_int64
+    assert f(boards[:100].ctypes.data, 100, 5, 3) == 0
+    if group > 1:  # and the solver's answers are the oracle's
+        lib = libs["plane_host"]
+        lib.plane_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                          ctypes.c_int, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p]
+        lib.plane_set_mrv_after.argtypes = [ctypes.c_uint32]
+        lib.plane_set_mrv_after(64)
+        sols, st = _solve(lib, boards)
+        want, cnt = O.solve_unique_batch(boards)
+        assert (cnt == 1).all() and (st == 1).all() and np.array_equal(sols, want)
 
 
 def test_open_root_rule_same_answers_fewer_passes(tmp_path):
