@@ -9,17 +9,16 @@ data-path collective).  A step = the hot path over one batch of B boards
 HBM.  --scaling strong (the default; BASELINE configs[2]: "1M ... sharded
 across 1/2/4/8 MI355X"): B boards per step over ALL ranks, rank r solving
 its shard_bounds share (B/N boards) of every step's batch; weak: B boards per
-GPU per step.  A shard of a step too small to fill the GPU alone (2^17 boards
-at N = 8) is launched together with the rank's next steps' shards --
-sdk_solve_batches, one queue over up to 32 batches that drains once -- until a
-launch holds --launch-boards (2^20) boards; each step's shard keeps its own
-input and output buffers.  Consecutive launches keep --inflight (default 6,
-with $GPU_MAX_HW_QUEUES = 8 set below) in flight per GPU, each on its own
-stream and workspace, each launch's grid holding --grid-waves (default 1)
-wave per SIMD (BatchSolver.solve_inflight): four launches are resident at
-once and the next ones fill their drains as their waves exit; `serial`
-reports the same steps back to back on full grids.  value = all
-ranks' boards / max-over-ranks wall time.
+GPU per step.  Launch plan "run" (the default): a rank's K timed steps are
+ceil(K / 32) sdk_solve_batches launches -- one queue over up to 32 steps'
+batches that drains once, on a full grid, the next launch queued behind the
+running one -- each step keeping its own input (the batch rotated by 7919 j
+boards for step j) and output buffers.  value = all ranks' boards /
+max-over-ranks wall time.  Beside it, labelled: `serial` = the same K steps
+as K one-step launches back to back, `single_batch` = one step's batch in
+one solve() call (the "1M batch" alone), `output_checks` = every timed
+step's output checked (SOLVED, Sudoku.check, givens kept, equal across the
+rotated steps).
 
 Rank 0 prints ONE JSON line with the contract fields plus:
   roofline     -- the solve kernel against the INT32 VALU roofline (VALU
@@ -68,6 +67,59 @@ def cpu_baseline(boards, budget_s: float):
     t0 = time.perf_counter()
     done = O.solve_batch_timed_parallel(boards, budget_s, threads)
     return done, time.perf_counter() - t0, threads
+
+
+ROTATION = 7919  # step j's batch is the synthetic batch rotated by ROTATION * j boards
+
+
+def run_plan(steps: int) -> dict:
+    """Launch plan "run" (the default) for `steps` timed steps: ceil(K / 32)
+    sdk_solve_batches launches of equal step counts on full grids, the
+    running launch and the next one queued behind it (two in flight), the
+    last launch sharing its tail through the XCD pool.  tests/test_gpu_full_size.py
+    diffs exactly this shape against the oracle."""
+    from sudoku_solver_distributed_amd._lib import SDK_MAX_BATCHES
+    n_launch = -(-steps // SDK_MAX_BATCHES)
+    return {"group": -(-steps // n_launch), "inflight": 2, "grid_waves": 0, "pool_last": 1}
+
+
+def step_inputs(full, lo: int, hi: int, group: int, dev):
+    """One input per step of a launch group: step j's boards are this rank's
+    [lo, hi) of the batch rotated by ROTATION * j boards."""
+    import torch
+    n = full.shape[0]
+    return [full[(torch.arange(lo, hi) + ROTATION * j) % n].contiguous().to(dev) for j in range(group)]
+
+
+def check_steps(solver, inputs, bufs, steps, group, lo, batch):
+    """Every buffer the timed steps wrote, against the reference's contract
+    (gen.py:6-28's first completion of every board): every board SOLVED and
+    passing Sudoku.check (sudoku.py:119-140), the givens kept, and -- step j
+    being the batch rotated by 7919 j boards -- board for board equal to the
+    answer another step gave the same global board (buffer b holds the last
+    step i < steps with i % len(bufs) == b)."""
+    import torch
+    nb = len(bufs)
+    shard = inputs[0].shape[0]
+    held = [max(i for i in range(steps) if i % nb == b) for b in range(min(nb, steps))]
+    ok = {"solved": True, "checked": True, "givens_kept": True, "rotations_agree": True}
+    ref_b = 0
+    j_ref = held[ref_b] % group
+    ar = torch.arange(shard, device=inputs[0].device)
+    for b, i in enumerate(held):
+        out, st = bufs[b]
+        inp = inputs[i % group]
+        ok["solved"] &= bool((st == 1).all())
+        ok["checked"] &= bool((solver.check(out, 0) == 1).all())
+        ok["givens_kept"] &= bool(((inp == 0) | (out == inp)).all())
+        # position k of step i is global board (lo + k + 7919 j) % batch; in
+        # the reference buffer it sits at (global - lo - 7919 j_ref) % batch
+        j = i % group
+        g = (lo + ar + ROTATION * j) % batch
+        k_ref = (g - lo - ROTATION * j_ref) % batch
+        sel = k_ref < shard
+        ok["rotations_agree"] &= bool(torch.equal(out[sel], bufs[ref_b][0][k_ref[sel]]))
+    return ok
 
 
 def _time(fn, reps=3):
@@ -400,7 +452,8 @@ def main():
                     help="passes on a board before its search switches to the completion count "
                          "(sdk_set_plane_search; -1: the library default, 0: the walk's order only) -- A/B only")
     ap.add_argument("--no-serial", action="store_true",
-                    help="skip the back-to-back comparison (profiling runs: only the timed launch shape runs)")
+                    help="skip the one-launch-per-step and single-batch figures (profiling runs: only the timed "
+                         "launch shape runs)")
     ap.add_argument("--no-serving", action="store_true",
                     help="skip the configs[4] HTTP serving figures (peers in this process and as processes)")
     ap.add_argument("--no-extras", action="store_true",
@@ -467,8 +520,7 @@ def main():
     plan_run = args.plan == "run" and args.launches <= 0 and args.launch_boards < 0
     if plan_run:
         # the whole run's steps in ceil(K / 32) launches of equal step counts
-        n_launch = -(-args.steps // SDK_MAX_BATCHES)
-        group = -(-args.steps // n_launch)
+        group = run_plan(args.steps)["group"]
     if args.launches > 0:
         group = min(SDK_MAX_BATCHES, -(-args.steps // args.launches))
     # one input per step of a launch group (each step its own boards): step
@@ -476,17 +528,14 @@ def main():
     # generation however many steps a launch holds); strong: this rank's
     # [lo, hi) of it (the same global batch on every rank), weak: per-rank seeds
     full = make(args.batch, seed=args.seed + (rank if args.scaling == "weak" else 0))
-    inputs = []
-    for j in range(group):
-        idx = (torch.arange(lo, hi) + 7919 * j) % args.batch
-        inputs.append(full[idx].contiguous().to(dev))
+    inputs = step_inputs(full, lo, hi, group, dev)
     del full
     boards = inputs[0]
     from sudoku_solver_distributed_amd.solver import default_inflight
     m_def, gw_def = default_inflight()
     m = m_def if args.inflight < 0 else max(1, args.inflight)
     if plan_run and args.inflight < 0:
-        m = 2  # the running launch and the next one queued behind it
+        m = run_plan(args.steps)["inflight"]  # the running launch and the next one queued behind it
     # one (solutions, status) pair per step that can be in flight: step i
     # reads inputs[i % group] and writes pair i % (m * group)
     nb = m * group
@@ -507,7 +556,7 @@ def main():
     # the launches that share their tails through the XCD pool (unpipelined):
     # plan run: the last (nothing is queued behind it); inflight: half the
     # launches in flight (solve_inflight's default)
-    pool_last_arg = args.pool_last if args.pool_last >= 0 else (1 if plan_run else None)
+    pool_last_arg = args.pool_last if args.pool_last >= 0 else (run_plan(args.steps)["pool_last"] if plan_run else None)
 
     def steps(k, events=None, inflight=m):
         solver.solve_inflight([inputs[i % group] for i in range(k)], [bufs[i % nb][0] for i in range(k)],
@@ -551,21 +600,45 @@ def main():
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
-    # every buffer a timed step wrote: all SOLVED, all pass Sudoku.check, and
-    # equal to the other buffers that hold the same input's answers
-    solved_ok = all(bool((bufs[i][1] == 1).all()) and bool((solver.check(bufs[i][0], 0) == 1).all())
-                    and bool(torch.equal(bufs[i][0], bufs[i % group][0])) for i in range(min(nb, args.steps)))
+    checks = check_steps(solver, inputs, bufs, args.steps, group, lo, args.batch)
+    solved_ok = all(checks.values())
 
-    # the same steps back to back (one launch in flight), for comparison
+    # the same K steps as K one-step launches back to back (each its own
+    # full grid and its own drain): what a run costs without plan "run"'s
+    # one queue over the steps
     serial = None
-    if m > 1 and not args.no_serial:
+    if not args.no_serial:
         torch.cuda.synchronize(dev)
         s0 = time.perf_counter()
-        steps(args.steps, inflight=1)
+        solver.solve_inflight([inputs[i % group] for i in range(args.steps)], [bufs[i % nb][0] for i in range(args.steps)],
+                              [bufs[i % nb][1] for i in range(args.steps)], inflight=1, grid_waves=0, group=1)
         torch.cuda.synchronize(dev)
         s_wall = time.perf_counter() - s0
         solver.verify_inflight()
-        serial = {"value": shard * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3}
+        serial = {"what": "the same steps, one launch per step, back to back (full grid each)",
+                  "value": shard * args.steps / s_wall, "ms_per_step": s_wall / args.steps * 1e3,
+                  "outputs_checked": all(check_steps(solver, inputs, bufs, args.steps, group, lo, args.batch).values())}
+
+    # one step's batch alone: one device-resident solve() call (this rank's
+    # shard of step 0, 2^20 boards at N = 1), best of 3
+    single = None
+    if not args.no_serial:
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        best = None
+        for _ in range(3):
+            torch.cuda.synchronize(dev)
+            s0 = time.perf_counter()
+            e0.record(stream)
+            solver.solve(inputs[0], out=bufs[0][0], status=bufs[0][1])
+            e1.record(stream)
+            torch.cuda.synchronize(dev)
+            w_ms = (time.perf_counter() - s0) * 1e3
+            k_ms = e0.elapsed_time(e1)
+            best = (w_ms, k_ms) if best is None or w_ms < best[0] else best
+        solver.verify()
+        single = {"what": "one batch alone: one solve() call of one step's boards, best of 3",
+                  "boards": shard, "wall_ms": best[0], "kernel_ms": best[1], "boards_per_s": shard / best[0] * 1e3,
+                  "all_solved": bool((bufs[0][1] == 1).all())}
 
     # single-board latency (p50 over 32 boards, one launch each)
     lat = []
@@ -694,7 +767,9 @@ def main():
                    "dist_backend": args.dist_backend if world > 1 else None,
                    **({"emulated_rank": job_rank, "emulated_world": job_world, "rank_wall_s": wall_max}
                       if emulated else {})},
-        "serial": serial,  # this GPU's steps back to back (rank 0's boards / s)
+        "serial": serial,  # this GPU's steps as one launch each, back to back (rank 0's boards / s)
+        "single_batch": single,  # one step's batch in one solve() call (rank 0)
+        "output_checks": checks,
         "p50_single_ms": p50,
         "all_solved_and_checked": solved_ok,
         "guesses_per_board": st["guesses"] / max(st["finished"], 1),

@@ -75,6 +75,9 @@
 #ifndef SDK_PLANE_STAMPS
 #define SDK_PLANE_STAMPS 0
 #endif
+#ifndef SDK_PLANE_LDS_PAD
+#define SDK_PLANE_LDS_PAD 0
+#endif
 static_assert(plane::STACK_ENTRY == 27, "stack layout");
 typedef uint32_t sdk_v4u __attribute__((ext_vector_type(4)));
 
@@ -804,6 +807,10 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&ws[WS_ASSIGNED], (unsigned long long)n);  // sdk_verify_workspace
     __shared__ __attribute__((aligned(16))) uint32_t stage_lds[PLANE_THREADS / 64][PLANE_STAGE_DWORDS];
     __shared__ __attribute__((aligned(16))) uint32_t outbox_lds[PLANE_THREADS / 64][PLANE_OUTBOX * PLANE_OB_WORDS];
+#if SDK_PLANE_LDS_PAD
+    __shared__ uint32_t lds_pad[PLANE_THREADS / 64][SDK_PLANE_LDS_PAD];  // A/B: occupancy by LDS
+    asm volatile("" ::"v"((uint32_t)(uintptr_t)&lds_pad[0][0]));
+#endif
     uint32_t *stage = stage_lds[threadIdx.x >> 6];
     uint32_t *outbox = outbox_lds[threadIdx.x >> 6];
     uint32_t ob_count = 0;  // boards waiting in the outbox (wave-uniform)

@@ -87,3 +87,41 @@ def test_bench_two_rank_path_runs():
     assert d["config"]["grid_waves_per_simd"] is None
     assert d["side_configs"]["pathological"]["ranks"] == 2 and d["side_configs"]["pathological"]["identical"]
     assert d["all_solved_and_checked"] and d["value"] > 0
+
+
+def test_check_steps_rotation_logic():
+    """bench.check_steps on CPU tensors: step j's batch is the global batch
+    rotated by 7919 j boards (this rank's [lo, hi) of it); outputs that
+    agree board for board across the rotations pass, a single wrong board in
+    any step, a changed given or a non-SOLVED status fails its check."""
+    import torch
+    import bench
+
+    class FakeSolver:
+        def check(self, grids, mode):
+            return torch.ones(grids.shape[0], dtype=torch.int32)
+
+    batch, group = 20_000, 5
+    g = torch.randint(1, 10, (batch, 81), dtype=torch.uint8)      # "answers" of the global boards
+    given = torch.rand(batch, 81) < 0.2
+    puzzles = torch.where(given, g, torch.zeros_like(g))
+    for lo, hi in ((0, batch), (5_000, 10_000)):
+        inputs, bufs = [], []
+        for j in range(group):
+            idx = (torch.arange(lo, hi) + 7919 * j) % batch
+            inputs.append(puzzles[idx])
+        for i in range(2 * group):
+            idx = (torch.arange(lo, hi) + 7919 * (i % group)) % batch
+            bufs.append((g[idx].clone(), torch.ones(hi - lo, dtype=torch.int32)))
+        fs = FakeSolver()
+        assert all(bench.check_steps(fs, inputs, bufs, 2 * group, group, lo, batch).values())
+        bufs[3][0][17, 4] ^= 1  # a wrong answer in one step
+        ok = bench.check_steps(fs, inputs, bufs, 2 * group, group, lo, batch)
+        assert not ok["rotations_agree"]
+        bufs[3][0][17, 4] ^= 1
+        k = int(torch.nonzero(inputs[2][0]).flatten()[0])
+        bufs[2][0][0, k] = 0 if bufs[2][0][0, k] else 1  # a changed given
+        assert not bench.check_steps(fs, inputs, bufs, 2 * group, group, lo, batch)["givens_kept"]
+        bufs[2][0][0, k] = inputs[2][0, k]
+        bufs[6][1][9] = 0
+        assert not bench.check_steps(fs, inputs, bufs, 2 * group, group, lo, batch)["solved"]

@@ -2,11 +2,14 @@
 board by board, and the workspace's own accounting of answered boards.
 
 * all 2^20 boards of the bench's batch (hard17_batch(2^20, seed 2024)) solved
-  by one call, and by the EXACT launch shape bench.py times (six launches in
-  flight, one wave per SIMD each, the last three sharing their tails through
-  the XCD pool, eight hardware queues): every board of every launch equal to
-  the oracle's unique completion (oracle_solve_unique_prop: 17-clue boards
-  have one completion, which is therefore the walk's first, gen.py:6-28);
+  by one call, and by the EXACT launch shape bench.py times (bench.run_plan,
+  bench.step_inputs: the driver's 20 steps, each the batch rotated by 7919 j
+  boards, as ONE sdk_solve_batches launch on a full grid, two launches in
+  flight, the XCD pool on the last), at N = 1 (20 x 2^20 boards) and for
+  rank 7 of the 8-GPU run (20 x 2^17): every board of every step equal to
+  the oracle's unique completion of the same global board
+  (oracle_solve_unique_prop: 17-clue boards have one completion, which is
+  therefore the walk's first, gen.py:6-28);
 * a pool consumer that gives up waiting on a record (forced: zero polls)
   makes sdk_verify_workspace raise, and a flag the abandoned launch left set
   never leaks into the next launch on the same workspace (generation-tagged
@@ -50,30 +53,60 @@ def test_full_size_vs_oracle(solver, full_batch):
     assert v["assigned"] == v["finished"] == N and v["error"] == 0
 
 
-def test_bench_launch_shape_vs_oracle(solver, full_batch):
-    """bench.py's timed shape: 6 copies of the 2^20 batch, six launches in
-    flight at one wave per SIMD, pool on the last three; all six outputs
-    byte-equal and equal to the oracle, every board answered once."""
-    from sudoku_solver_distributed_amd.solver import default_inflight, pipelined_launches
-    assert os.environ.get("GPU_MAX_HW_QUEUES") == "8"   # conftest: as bench.py
-    inflight, gw = default_inflight()
-    assert (inflight, gw) == (6, 1)
-    assert pipelined_launches(6, 6, 3) == [True, True, True, False, False, False]
+def _timed_shape_vs_oracle(solver, full_batch, world, rank, steps=20):
+    """bench.py's timed launch shape, verbatim (bench.run_plan / step_inputs,
+    the calls bench.main makes): `steps` steps, step j = this rank's
+    shard_bounds slice of the 2^20 batch rotated by 7919 j boards, one
+    sdk_solve_batches launch over all of them (group = steps), two in
+    flight, full grid, the pool on the last launch.  Every board of every
+    step equal to the oracle's answer for the same global board, every
+    status SOLVED, every board answered exactly once."""
+    import bench
+    from sudoku_solver_distributed_amd.distributed import shard_bounds
     p, want = full_batch
-    d = p.cuda()
-    outs = [torch.full_like(d, 0xEE) for _ in range(6)]
-    sts = [torch.full((N,), 77, dtype=torch.int32, device=d.device) for _ in range(6)]
-    solver._slot_solvers(6)
+    lo, hi = shard_bounds(N, rank, world)
+    shard = hi - lo
+    plan = bench.run_plan(steps)
+    assert plan == {"group": steps, "inflight": 2, "grid_waves": 0, "pool_last": 1}
+    g = plan["group"]
+    dev = torch.device("cuda", 0)
+    inputs = bench.step_inputs(p, lo, hi, g, dev)
+    nb = plan["inflight"] * g
+    outs = [torch.full((shard, 81), 0xEE, dtype=torch.uint8, device=dev) for _ in range(nb)]
+    sts = [torch.full((shard,), 77, dtype=torch.int32, device=dev) for _ in range(nb)]
+    solver._slot_solvers(plan["inflight"])
     solver.inflight_stats(reset=True)
-    solver.solve_inflight([d] * 6, outs, sts, inflight=6, grid_waves=1, pool_last=3)
+    solver.verify_inflight()
+    solver.solve_inflight([inputs[i % g] for i in range(steps)], [outs[i % nb] for i in range(steps)],
+                          [sts[i % nb] for i in range(steps)], inflight=plan["inflight"],
+                          grid_waves=plan["grid_waves"], group=g, pool_last=plan["pool_last"])
     torch.cuda.synchronize()
     v = solver.verify_inflight()
-    assert v["assigned"] == v["finished"] == 6 * N and v["error"] == 0
-    assert solver.inflight_stats()["finished"] == 6 * N
-    for i in range(6):
+    assert v["assigned"] == v["finished"] == steps * shard and v["error"] == 0
+    assert solver.inflight_stats()["finished"] == steps * shard
+    want_d = torch.from_numpy(want).to(dev)
+    for i in range(steps):
+        idx = (torch.arange(lo, hi, device=dev) + bench.ROTATION * (i % g)) % N
         assert bool((sts[i] == 1).all()), i
-        assert torch.equal(outs[i], outs[0]), i
-    assert np.array_equal(outs[0].cpu().numpy(), want)
+        assert torch.equal(outs[i], want_d[idx]), i
+    # the bench's own check of the same buffers agrees
+    ok = bench.check_steps(solver, inputs, [(outs[i], sts[i]) for i in range(nb)], steps, g, lo, N)
+    assert all(ok.values()), ok
+    for i in range(steps, nb):  # buffers no step wrote stay untouched
+        assert bool((sts[i] == 77).all())
+
+
+def test_bench_timed_shape_vs_oracle(solver, full_batch):
+    """The driver's N = 1 command (--steps 20): 20 rotated copies of the 2^20
+    batch, 21 M boards through ONE plane_kernel_multi launch, diffed board by
+    board against the oracle (gen.py:6-28's first completion of each)."""
+    _timed_shape_vs_oracle(solver, full_batch, world=1, rank=0)
+
+
+def test_bench_rank_shape_vs_oracle(solver, full_batch):
+    """One rank of the 8-GPU strong-scaling run: rank 7's 2^17-board shard
+    of each of the 20 rotated steps in one launch, against the oracle."""
+    _timed_shape_vs_oracle(solver, full_batch, world=8, rank=7)
 
 
 _TIMEOUT_CHILD = r"""
