@@ -220,7 +220,10 @@ PS_FN int pass(Board &B, uint32_t und[3])
     const bool any_nd = or3(nd[0], nd[1], nd[2]) != 0;
     pin_board(B);
 
-    uint32_t hall[3] = {0u, 0u, 0u}, hgrp[3] = {0u, 0u, 0u};
+    uint32_t hall[3] = {0u, 0u, 0u};
+#if SDK_PLANE_GROUP > 1
+    uint32_t hgrp[3] = {0u, 0u, 0u};
+#endif
     // per unit kind, "d has a place": row guard bits, columns, box bits 0/3/6
     uint32_t rowall = GUARDS, colall = 0x1FFu, boxall = BOXC;
 #pragma unroll
@@ -231,7 +234,11 @@ PS_FN int pass(Board &B, uint32_t und[3])
         uint32_t x[3], f[3];
 #pragma unroll
         for (int b = 0; b < 3; ++b) {
+#if SDK_PLANE_GROUP > 1
             if (d >= SDK_PLANE_GROUP) B.P[d][b] = andn(B.P[d][b], hgrp[b]);
+#else
+            if (d > 0) B.P[d][b] = andn(B.P[d][b], hall[b]);  // (the same code path as before groups existed)
+#endif
             x[b] = nd[b] & B.P[d][b];
             f[b] = or3(x[b], x[b] >> 10, x[b] >> 20);  // bits 0-8: columns holding x (above: junk)
         }
@@ -324,9 +331,11 @@ PS_FN int pass(Board &B, uint32_t und[3])
 #endif
             hall[b] = or_and(hall[b], B.P[d][b], hs);
         }
+#if SDK_PLANE_GROUP > 1
         if (d % SDK_PLANE_GROUP != SDK_PLANE_GROUP - 1 && d != 8) continue;
 #pragma unroll
         for (int b = 0; b < 3; ++b) hgrp[b] = hall[b];  // what the next group's digits drop first
+#endif
         pin_board(B);
         // the unit accumulators too: unpinned, the AND / OR chains over the
         // nine digits are re-associated into trees at the end of the pass,
