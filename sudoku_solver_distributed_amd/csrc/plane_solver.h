@@ -698,6 +698,16 @@ enum { S_CONT = 0, S_SOLVED = 1, S_NONE = 2, S_DEEP = 3 };
 #ifndef SDK_PLANE_ROOT_OPEN
 #define SDK_PLANE_ROOT_OPEN 58
 #endif
+// A backtrack that takes a level's LAST untried digit leaves the level
+// exhausted: with SDK_PLANE_LASTPOP the search then continues at that
+// level's depth (the next guess overwrites its line) instead of one deeper,
+// so its entry is not rewritten and a later backtrack does not load it to
+// find nothing there.  Level 0 is kept (it holds the propagated root the
+// completion count and the final walk restart from).  The visiting order --
+// and so every answer -- is the same; only the stack levels in use shrink.
+#ifndef SDK_PLANE_LASTPOP
+#define SDK_PLANE_LASTPOP 1
+#endif
 PS_FN bool root_counts(int mode, uint32_t depth, uint32_t mrv_after, uint32_t u0, uint32_t u1, uint32_t u2)
 {
     return SDK_PLANE_ROOT_OPEN && mrv_after && mode == M_WALK && depth == 0 &&
@@ -727,7 +737,7 @@ PS_FN int search_step(Board &B, const uint32_t (&und)[3], int r, uint32_t &depth
     // a kept completion (one site keeps the kernel's registers in bounds)
     int reload = -1, save = -1;  // and the one plane store: a guess's level, or the kept completion
     uint32_t save_entry = 0;
-    bool fix = false, fresh = false;
+    bool fix = false, fresh = false, last = false;
     int fix_band = 0, fix_pos = 0, res = S_CONT;
     uint32_t fix_d = 0;
     if (mode == M_WALK && mrv_after && r != SOLVED && (mst & MST_PASSES) >= mrv_after) {
@@ -787,7 +797,11 @@ PS_FN int search_step(Board &B, const uint32_t (&und)[3], int r, uint32_t &depth
         const uint32_t rem = (e >> 8) & 0x1FFu;
         if (rem) {
             fix_d = rem & (0u - rem);
-            stk.put_entry((uint32_t)reload, e & ~(fix_d << 8));
+#if SDK_PLANE_LASTPOP
+            last = rem == fix_d && reload > 0;  // the level's last digit: continue at its depth, entry untouched
+            if (!last)
+#endif
+                stk.put_entry((uint32_t)reload, e & ~(fix_d << 8));
             fix_band = (int)((e >> 5) & 3u);
             fix_pos = (int)(e & 31u);
             depth = (uint32_t)reload;
@@ -809,7 +823,7 @@ PS_FN int search_step(Board &B, const uint32_t (&und)[3], int r, uint32_t &depth
     // set_cell for both groups of lanes (the wave runs both paths in most
     // iterations)
     if (fix) {
-        depth++;
+        depth += last ? 0u : 1u;
         guesses++;
         set_cell(B, fix_band, fix_pos, fix_d);
     }

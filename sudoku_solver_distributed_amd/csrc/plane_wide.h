@@ -458,8 +458,15 @@ WD_FN int solve(V &w, uint32_t &depth, const Stack &stk, const Lanes &L, int nod
             const uint32_t dbit = rem & (0u - rem);
             w = stk.restore(depth, L);
             det = V(0u);
+#if SDK_PLANE_LASTPOP
+            if (rem != dbit || depth == 0) {  // (a level's last digit: continue at its depth, plane_solver.h)
+                stk.put_entry(depth, e & ~(dbit << 8));
+                depth++;
+            }
+#else
             stk.put_entry(depth, e & ~(dbit << 8));
             depth++;
+#endif
             st.guesses++;
             st.bguess++;
             set_cell(w, L, (int)((e >> 5) & 3u), (int)(e & 31u), dbit);
