@@ -148,8 +148,13 @@ class GpuSolverBackend:
         for i in range(k):
             want = (i + 1) * n // k - i * n // k
             if want and int(counts[i, 0]) != want:
-                raise SudokuHipError(f"solver {i}: {int(counts[i, 0])} of {want} boards answered "
-                                     f"({self.solvers[i].verify()})")
+                # verify() raises its own error (and clears the workspace's
+                # error word): keep its text and this batch's shortfall together
+                try:
+                    detail = f"workspace: {self.solvers[i].verify()}"
+                except SudokuHipError as e:
+                    detail = str(e)
+                raise SudokuHipError(f"solver {i}: {int(counts[i, 0])} of {want} boards answered ({detail})")
         return out, st, int(counts[:, 3].sum())
 
     def peer_solve(self, boards: torch.Tensor):
