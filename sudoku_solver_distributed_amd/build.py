@@ -17,10 +17,16 @@ ROOT = os.path.dirname(_HERE)
 _SCHED = os.environ.get("SDK_PLANE_SCHED", "iterative-ilp")
 
 
+# SDK_PLANE_LLVM: more LLVM options for the plane unit (space-separated, each
+# passed through -mllvm; A/B builds of the code generator only)
+_LLVM_EXTRA = os.environ.get("SDK_PLANE_LLVM", "").split()
+
+
 def sources(sched: str = _SCHED):
     """Translation units and their flags for one plane-unit scheduler."""
+    extra = [f for o in _LLVM_EXTRA for f in ("-mllvm", o)]
     return (("sudoku_kernels.hip", []),
-            ("plane_kernels.hip", [] if sched == "default" else ["-mllvm", f"-amdgpu-sched-strategy={sched}"]))
+            ("plane_kernels.hip", ([] if sched == "default" else ["-mllvm", f"-amdgpu-sched-strategy={sched}"]) + extra))
 
 
 SRCS = sources()
