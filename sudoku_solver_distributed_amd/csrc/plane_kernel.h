@@ -306,7 +306,13 @@ struct PlaneIOn {
 // >= (3 + 64*81 + 3) / 4 rounded up to 64 (the span DMA writes whole 64-dword
 // rows), plus one dword the DMA never writes: a zero byte for the refill's
 // cell-less slots (byte offset PLANE_STAGE_ZERO, zeroed at kernel start)
-enum { PLANE_STAGE_DWORDS = 1348, PLANE_STAGE_ZERO = 4 * (PLANE_STAGE_DWORDS - 1) };
+// (a five-waves-per-SIMD budget, <= 8 KB of LDS per wave with 48-board
+// claims, a 56-board outbox and two start-up spans, measured -4 % / -9 % at
+// N = 1 / 8: the 96-VGPR limit spills 30 registers in the lane loop)
+enum {
+    PLANE_STAGE_DWORDS = 1348, PLANE_STAGE_ZERO = 4 * (PLANE_STAGE_DWORDS - 1),
+    PLANE_START_SPAN = 64  // boards per staged span at start-up
+};
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 // s_waitcnt immediates (gfx9: vmcnt bits 3:0 + 15:14, expcnt 6:4, lgkmcnt 11:8)
@@ -372,7 +378,9 @@ __device__ __forceinline__ void plane_stage_words(const uint32_t *stage, uint32_
 // refill then hands record i to the idle lane of rank i: every loaded lane
 // reads its own record at once, no per-board serial work.
 enum { PLANE_REC = 13, PLANE_CHUNK_MAX = 64 };
-static_assert(64 * PLANE_REC + 1 < PLANE_STAGE_DWORDS, "chunk records");
+static_assert(PLANE_CHUNK_MAX * PLANE_REC + 1 < PLANE_STAGE_DWORDS, "chunk records");
+static_assert((3 + 81 * PLANE_CHUNK_MAX + 3 + 255) / 256 * 64 < PLANE_STAGE_DWORDS, "a claimed chunk's span");
+static_assert((3 + 81 * PLANE_START_SPAN + 3 + 255) / 256 * 64 < PLANE_STAGE_DWORDS, "a start-up span");
 
 __device__ __forceinline__ void plane_convert_chunk(uint32_t *stage, uint32_t sh, int count, int lane)
 {
@@ -862,42 +870,17 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     uint64_t st_claims = 0;                         // queue claims: count | last size << 32
 #endif
 
-    // Start-up: the wave's first 64 boards arrive as one staged span; each
-    // lane then converts its own board (plane::load_words), all lanes at once.
-    if constexpr (!IO::multi) {
-        const unsigned long long base = (unsigned long long)(g - lane);
-        queue_out = nt >= n;
-        drained = queue_out;
-        const int64_t q = (int64_t)base + lane;
-        const int64_t kk = (int64_t)base < n ? (n - (int64_t)base < 64 ? n - (int64_t)base : 64) : 0;
-        const uint32_t sh = kk ? plane_stage_span(io.in, n, (int64_t)base, (int)kk, stage, lane) : 0u;
-        if (q < n) {
-            const uint8_t *src = io.src(q);
-            uint32_t x[21];
-            plane_stage_words(stage, sh + 81u * (uint32_t)lane, x);
-            bool clash;  // tested lazily (see the unsolvable store above)
-            const bool ok = plane::load_words(B, x, clash);
-            const bool cancel = ok && best && __hip_atomic_load(best, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < q;
-            if (ok && !cancel) {
-                p = q;
-                depth = 0;
-                bguess = 0;
-                mst = 0;
-                state = PL_ACTIVE;
-            } else {
-                for (int i = 0; i < 81; ++i) io.out[q * 81 + i] = src[i];  // raw input back
-                *io.stat(q) = ok ? SDK_CANCELLED : SDK_INVALID;
-                fin++;  // (a board counts as finished when its answer is written)
-            }
-        }
-    } else {
+    // Start-up: the wave's first 64 boards arrive as staged spans (one per
+    // batch segment of the window, at most PLANE_START_SPAN boards each);
+    // each lane then converts its own board (plane::load_words), all at once.
+    {
         const int64_t v0 = g - lane;
         queue_out = nt >= n;
         drained = queue_out;
         const int64_t kk = v0 < n ? (n - v0 < 64 ? n - v0 : 64) : 0;
-        // one staged span per batch segment of the window (one for one batch)
         for (int64_t s0 = 0; s0 < kk;) {
-            const int64_t sv = v0 + s0, se = io.seg_end(sv, v0 + kk);
+            const int64_t sv = v0 + s0, cap = sv + PLANE_START_SPAN < v0 + kk ? sv + PLANE_START_SPAN : v0 + kk;
+            const int64_t se = io.seg_end(sv, cap);
             const int cnt = (int)(se - sv);
             const uint32_t sh = plane_stage_span(io.seg_in(sv), io.seg_n(sv), io.seg_local(sv), cnt, stage, lane);
             const int r = lane - (int)s0;
@@ -919,10 +902,12 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     uint8_t *dst = io.dst(q);
                     for (int i = 0; i < 81; ++i) dst[i] = src[i];  // raw input back
                     *io.stat(q) = ok ? SDK_CANCELLED : SDK_INVALID;
-                    fin++;
+                    fin++;  // (a board counts as finished when its answer is written)
                 }
             }
             s0 = se - v0;
+            // the next span's DMA overwrites the stage: every lane has its words
+            if (s0 < kk) wave_lds_sync();
         }
     }
 
@@ -1030,8 +1015,8 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     c = c > chunk ? chunk : c;
                     // a chunk is staged and converted in one go: at most 64 records
                     // fit the staging area (the host also rejects chunk > 64)
-                    c = c > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : c;
                     c = c < k ? k : c;
+                    c = c > PLANE_CHUNK_MAX ? PLANE_CHUNK_MAX : c;  // (then some idle lanes wait a pass)
                     if (lane == leader) base = atomicAdd(&ws[WS_QUEUE], (unsigned long long)c);
 #if SDK_PLANE_STAMPS
                     st_claims = ((st_claims & 0xFFFFFFFFull) + 1) | ((uint64_t)c << 32);  // count, last size
