@@ -724,7 +724,7 @@ def main():
             roof["useful_lane_frac"] = useful / ops
             roof["useful_frac_of_peak"] = useful / kern_s / 1e12 / roof["peak"]
         # the pass's own ceiling at the kernel's occupancy (microbenchmark)
-        ceil = os.path.join(PMC_DIR, "r05_pass_ceiling.json")
+        ceil = os.path.join(PMC_DIR, "r06_pass_ceiling.json")
         if kname.startswith("plane_kernel") and os.path.exists(ceil):
             with open(ceil) as f:
                 c = json.load(f)

@@ -4,11 +4,13 @@ Bar: bit-exact boards and statuses.  The full-size cases (BASELINE.json's 1M
 hard batch, every board against the oracle, and the bench's exact launch
 shape) are in test_gpu_full_size.py.
 """
+import os
+
 import numpy as np
 import pytest
 import torch
 
-from conftest import b81, load_golden
+from conftest import GOLDEN, b81, load_golden
 from oracle import oracle as O
 
 pytestmark = pytest.mark.gpu
@@ -44,13 +46,20 @@ def test_golden_named(solver):
 
 @pytest.mark.parametrize("order", ["gen", "node"])
 def test_random_generated_vs_oracle(solver, order):
+    """Seeded generate_batch boards, 30-81 empties, against the oracle's
+    literal walk in each order.  The walk's answers are the committed fixture
+    (tests/golden/make_random_generated.py; a few of these boards keep the
+    literal walk busy for up to a minute each, so the fixture is pinned to
+    the oracle on the CPU suite: test_oracle.py::test_random_generated_fixture)."""
     from sudoku_solver_distributed_amd.gen import generate_batch
-    for empties, n in ((30, 256), (50, 256), (58, 256), (64, 128), (70, 64), (81, 4)):
-        puzzles = generate_batch(n, empties, seed=1234 + empties)
+    z = np.load(os.path.join(GOLDEN, "random_generated.npz"))
+    for empties, n in z["cases"]:
+        empties, n = int(empties), int(n)
+        puzzles = generate_batch(n, empties, seed=int(z["seed0"]) + empties)
+        assert np.array_equal(puzzles.cpu().numpy(), z[f"puzzles_{empties}"]), empties
         sols, st = solver.solve(puzzles, order=order)
-        want, wst = O.solve_batch(puzzles.cpu().numpy(), order=order)
-        assert np.array_equal(st.cpu().numpy(), wst), empties
-        assert np.array_equal(sols.cpu().numpy(), want), empties
+        assert np.array_equal(st.cpu().numpy(), z[f"{order}_status_{empties}"]), empties
+        assert np.array_equal(sols.cpu().numpy(), z[f"{order}_solutions_{empties}"]), empties
 
 
 def test_generate_batch_matches_sequential(solver):
