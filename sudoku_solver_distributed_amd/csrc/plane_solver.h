@@ -158,6 +158,25 @@ PS_FN uint32_t sel(uint32_t m, uint32_t a, uint32_t b) { return PS_BOP3(0xCA, m,
 PS_FN uint32_t bop3_nor(uint32_t a, uint32_t b, uint32_t c) { return PS_BOP3(0xEF, a, b, c, ~a | b | c); }
 // 9-bit set (low 24 bits of c may hold no other bit) times k: one v_mul_u32_u24
 PS_FN uint32_t mul24(uint32_t c, uint32_t k) { return (c & 0xFFFFFFu) * k; }
+// box bits (0 / 3 / 6, nothing else below bit 16) -> the boxes' nine
+// columns.  SDK_PLANE_MUL16: as a 16-bit multiply (v_mul_lo_u16 issues at
+// full rate on gfx950, v_mul_u32_u24 at half: profiles/r02_valu_rates.json)
+#ifndef SDK_PLANE_MUL16
+#define SDK_PLANE_MUL16 1
+#endif
+PS_FN uint32_t box_cols(uint32_t c)
+{
+#if SDK_PLANE_MUL16 && defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+    // in place: the high half of the register is c's (zero) whether the
+    // instruction keeps or clears it (LLVM itself widens the i16 multiply
+    // back to v_mul_u32_u24)
+    uint32_t r = c;
+    asm("v_mul_lo_u16 %0, 7, %0" : "+v"(r));
+    return r;
+#else
+    return mul24(c, 7u);
+#endif
+}
 
 // rule D, box -> row, on one band word y of a digit's plane: the cells to
 // clear because a box of the band holds all its places in one row -- that
@@ -275,7 +294,7 @@ PS_FN int pass(Board &B, uint32_t und[3])
             hb[b] = mul24(q, 0x701C07u);
 #if SDK_PLANE_LC
             const uint32_t vb = andn(xor3(o[b], o1, o2), mo) & BOXC;  // boxes with exactly one column
-            vp[b] = o[b] & mul24(vb, 7u);
+            vp[b] = o[b] & box_cols(vb);
 #endif
         }
         const uint32_t O = or3(o[0], o[1], o[2]);
