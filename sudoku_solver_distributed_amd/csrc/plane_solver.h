@@ -83,6 +83,18 @@
 #ifndef SDK_PLANE_GROUP
 #define SDK_PLANE_GROUP 1
 #endif
+// rule C's box singles through rule D's one-column boxes: a box with one
+// place is a box with one column (vp) whose column holds one place, and
+// that column's cells in the band stand for the box's; the box and column
+// singles then share one spread over the rows (27 multiplies and ~80 VALU
+// fewer per pass; same hidden singles).  Needs rule D's box -> column form.
+#ifndef SDK_PLANE_HX
+#define SDK_PLANE_HX 1
+#endif
+#if SDK_PLANE_HX && !(SDK_PLANE_LC & 1)
+#undef SDK_PLANE_HX
+#define SDK_PLANE_HX 0
+#endif
 
 namespace plane {
 
@@ -164,6 +176,15 @@ PS_FN uint32_t mul24(uint32_t c, uint32_t k) { return (c & 0xFFFFFFu) * k; }
 #ifndef SDK_PLANE_MUL16
 #define SDK_PLANE_MUL16 1
 #endif
+// the box bits of x & ~m: one v_bitop3 with BOXC in a VGPR instead of two ops
+PS_FN uint32_t box_one(uint32_t x, uint32_t m)
+{
+#if defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
+    return bop3<0x20>(x, m, vconst<BOXC>());
+#else
+    return x & ~m & BOXC;
+#endif
+}
 PS_FN uint32_t box_cols(uint32_t c)
 {
 #if SDK_PLANE_MUL16 && defined(__HIPCC__) && defined(__HIP_DEVICE_COMPILE__)
@@ -288,20 +309,36 @@ PS_FN int pass(Board &B, uint32_t und[3])
             const uint32_t o1 = o[b] >> 1, o2 = o[b] >> 2;
             const uint32_t ob = or3(o[b], o1, o2);     // box bits 0/3/6: >= 1 place
             boxall &= ob;
-            const uint32_t tb = or3(t[b], t[b] >> 1, t[b] >> 2);
             const uint32_t mo = maj3(o[b], o1, o2);     // box bits: >= 2 columns with a place
+#if SDK_PLANE_HX
+            // a box with one place: its one column (vp) holding one place
+            // (not in t); that column within the band lies in the box, so
+            // the column's three cells stand for the box's nine (below)
+            const uint32_t vb = box_one(xor3(o[b], o1, o2), mo);  // boxes with exactly one column
+            vp[b] = o[b] & box_cols(vb);
+            hb[b] = andn(vp[b], t[b]);
+#else
+            const uint32_t tb = or3(t[b], t[b] >> 1, t[b] >> 2);
             const uint32_t q = andn2(ob, tb, mo) & BOXC;  // boxes with exactly one
             hb[b] = mul24(q, 0x701C07u);
 #if SDK_PLANE_LC
             const uint32_t vb = andn(xor3(o[b], o1, o2), mo) & BOXC;  // boxes with exactly one column
             vp[b] = o[b] & box_cols(vb);
 #endif
+#endif
         }
         const uint32_t O = or3(o[0], o[1], o[2]);
         colall &= O;
         const uint32_t mo3 = maj3(o[0], o[1], o[2]);  // columns with places in >= 2 bands
         const uint32_t hc = andn2(O, or3(t[0], t[1], t[2]), mo3) & 0x1FFu;
+#if SDK_PLANE_HX
+        // box and column singles share one spread over the band's rows
+#pragma unroll
+        for (int b = 0; b < 3; ++b) hb[b] = mul24(hb[b] | hc, 0x100401u);
+        const uint32_t hcol = 0u;
+#else
         const uint32_t hcol = mul24(hc, 0x100401u);
+#endif
         // d's hidden singles: the cells of y alone in their row, column or
         // box.  Later digits drop these cells at their turn (above), earlier
         // ones after the loop.  A cell forced for two digits loses the later
