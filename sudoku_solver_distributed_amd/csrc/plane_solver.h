@@ -232,9 +232,6 @@ PS_FN int pass(Board &B, uint32_t und[3])
 {
     uint32_t single[3], nd[3];
     uint32_t dead = 0;
-#if SDK_PLANE_LC
-    uint32_t lc = 0;  // rule D removed a place
-#endif
     // ---- A: determined cells.  o: >= 1 candidate, t: >= 2 candidates
 #pragma unroll
     for (int b = 0; b < 3; ++b) {
@@ -368,7 +365,6 @@ PS_FN int pass(Board &B, uint32_t und[3])
                 }
 #endif
                 const uint32_t e = mul24(ec, 0x100401u);
-                lc = or_and(lc, B.P[d][b], e);
                 B.P[d][b] = andn(B.P[d][b], e);
             }
         }
@@ -400,9 +396,6 @@ PS_FN int pass(Board &B, uint32_t und[3])
         PS_PIN(rowall);
         PS_PIN(colall);
         PS_PIN(boxall);
-#if SDK_PLANE_LC
-        PS_PIN(lc);
-#endif
 #pragma unroll
         for (int b = 0; b < 3; ++b) PS_PIN(hall[b]);
 #endif
@@ -429,10 +422,8 @@ PS_FN int pass(Board &B, uint32_t und[3])
 #pragma unroll
             for (int b = 0; b < 3; ++b) {
                 const uint32_t e = point_rows(B.P[d][b]);
-                lc = or_and(lc, B.P[d][b], e);
                 B.P[d][b] = andn(B.P[d][b], e);
                 PS_PIN(B.P[d][b]);
-                PS_PIN(lc);
             }
     }
 #endif
@@ -440,9 +431,10 @@ PS_FN int pass(Board &B, uint32_t und[3])
     if (dead) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = or3(hall[0] & und[0], hall[1] & und[1], hall[2] & und[2]) != 0;
-#if SDK_PLANE_LC
-    if (lc) return OPEN;
-#endif
+    // (rule D's removals alone do not make the pass OPEN: the board then
+    // branches one pass early, on sound planes -- host model: 21.389 against
+    // 21.390 passes per board, DESIGN.md §4 -- and the step saves its
+    // change tracking, 27 VALU)
     return (any_nd || newh) ? OPEN : STUCK;
 }
 

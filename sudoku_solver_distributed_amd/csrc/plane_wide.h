@@ -315,7 +315,6 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
         w = sel(or3(rn2 - (rn2 >> 9), cp2, mul24(g2 & BOXC, 0x701C07u)), x2, w);
     }
 #endif
-    bool lc = false;
 #if SDK_WIDE_LC
     {
         // ---- D (plane::pass rule D): a box whose places lie in one column
@@ -337,7 +336,6 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
 #if SDK_WIDE_LC & 2
         e = e | point_rows(w);
 #endif
-        lc = ballot(ne(w & e, V(0u))) != 0;
         w = andn(w, e);
     }
 #endif
@@ -345,7 +343,7 @@ WD_FN int pass(V &w, V &det, V &und, const Lanes &L)
     if (ballot(dead)) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = ballot(ne(H & und, V(0u))) != 0;
-    return (any_nd || newh || lc) ? OPEN : STUCK;
+    return (any_nd || newh) ? OPEN : STUCK;  // (rule D alone: not OPEN, as plane::pass)
 }
 
 // fix the cell (band, pos) to digit bit dbit

@@ -133,7 +133,7 @@ static uint32_t rnz(uint32_t y) { return (y + ROWS) & GUARDS; }
 static uint32_t fold(uint32_t y) { return (y | (y >> 10) | (y >> 20)) & 0x1FFu; }
 static int pass(Board &B, uint32_t und[3])
 {
-    uint32_t single[3], nd[3], dead = 0, lc = 0;
+    uint32_t single[3], nd[3], dead = 0;
     for (int b = 0; b < 3; ++b) {
         uint32_t o = 0, t = 0;
         for (int d = 0; d < 9; ++d) {
@@ -215,10 +215,6 @@ static int pass(Board &B, uint32_t und[3])
                 if ((claimed >> (3 * j)) & 7u) ec |= (7u << (3 * j)) & ~claimed;
 #endif
             uint32_t m = spread(ec);
-            lc |= B.P[d][b] & m;
-            B.P[d][b] &= ~m;
-            m = 0;
-            lc |= B.P[d][b] & m;
             B.P[d][b] &= ~m;
         }
 #endif
@@ -252,7 +248,6 @@ static int pass(Board &B, uint32_t und[3])
             }
             for (int k = 0; k < 3; ++k)
                 if (into[k]) m |= (0x1FFu & ~into[k]) << (10 * k);
-            lc |= B.P[d][b] & m;
             B.P[d][b] &= ~m;
         }
 #endif
@@ -260,7 +255,7 @@ static int pass(Board &B, uint32_t und[3])
     if (dead) return DEAD;
     if (all_single) return SOLVED;
     const bool newh = ((hall[0] & und[0]) | (hall[1] & und[1]) | (hall[2] & und[2])) != 0;
-    return (any_nd || newh || lc) ? OPEN : STUCK;
+    return (any_nd || newh) ? OPEN : STUCK;  // (rule D alone does not count, as plane::pass)
 }
 }  // namespace v1
 

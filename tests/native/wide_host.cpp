@@ -148,8 +148,10 @@ extern "C" void wide_solve_batch(const uint8_t *in, uint8_t *out, int32_t *statu
 
 // Fixpoints of the wide pass against the lane pass, from each loaded board
 // and from `trials` random mid-search states per board (random cells fixed to
-// a random candidate between propagations).  Both passes are iterated to
-// their first non-OPEN result.  Returns the number of states where the two
+// a random candidate between propagations).  Both passes are iterated until
+// the state stops changing (a STUCK pass may still have removed places by
+// rule D, which neither pass counts as progress; the orders differ, the
+// closure does not).  Returns the number of states where the two
 // disagree (verdict, planes or undetermined cells) and the STUCK side holds
 // no two determined cells with one digit in a unit: such a pair is a
 // contradiction neither rule set flags at once, and which pass meets it
@@ -199,8 +201,20 @@ extern "C" int64_t wide_check_fixpoint(const uint8_t *in, int64_t n, int trials,
             for (int k = 0; k < 64; ++k)
                 if (L.b.x[k] < 3) det.x[k] = B.Det[L.b.x[k]];
             int rw;
-            while ((rl = plane::pass(B, ul)) == plane::OPEN) {}
-            while ((rw = wide::pass(w, det, und, L)) == wide::OPEN) {}
+            for (;;) {
+                const plane::Board prev = B;
+                rl = plane::pass(B, ul);
+                if (rl == plane::OPEN || (rl == plane::STUCK && memcmp(prev.P, B.P, sizeof B.P) != 0)) continue;
+                break;
+            }
+            for (;;) {
+                const wide::V prev = w;
+                rw = wide::pass(w, det, und, L);
+                bool moved = false;
+                for (int k = 0; k < 64; ++k) moved |= prev.x[k] != w.x[k];
+                if (rw == wide::OPEN || (rw == wide::STUCK && moved)) continue;
+                break;
+            }
             bool diff = rl != rw;
             if (!diff && rl == plane::STUCK) {
                 const wide::V want = to_wave(B, L);
