@@ -272,12 +272,12 @@ def test_wide_edge_cases(wide):
     assert st[0] == 2
 
 
-# ---- split counting over an emulated tail pool (plane_kernel.h PoolHook)
+# ---- other pass variants
 
-@pytest.mark.parametrize("flags,group", [(0, 1), (3, 1), (5, 1), (7, 1), (1, 2), (1, 3), (1, 9), (7, 2)])
+@pytest.mark.parametrize("flags,group", [(0, 1), (1, 1), (5, 1), (7, 1), (3, 2), (3, 3), (3, 9), (7, 2)])
 def test_pass_variants_match_their_restatement(tmp_path, flags, group):
-    """Every SDK_PLANE_LC rule-D variant (0 none, 1 box -> column -- the
-    default, covered above --, 2 box -> row, 4 column -> box) and every
+    """Every SDK_PLANE_LC rule-D variant (0 none, 1 box -> column, 2 box ->
+    row -- 3, both, is the default, covered above --, 4 column -> box) and every
     SDK_PLANE_GROUP grouping of rule C's hidden singles (1 Gauss-Seidel, the
     default; 2 and 3 digits per group; 9 Jacobi) keeps the pass equal to its
     plain-loop restatement (plane_host.cpp v1::pass) after every pass, and
