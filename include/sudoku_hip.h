@@ -221,7 +221,7 @@ int sdk_set_plane_tuning(int refill, int tail, int tail_mode, int chunk);
  * branch order.  With the switch on, a board whose
  * propagated root keeps >= 58 open cells counts from the root at once.  0
  * keeps every board on the walk's order; -1
- * restores the default ($SDK_PLANE_MRV, built-in 64).  Results never
+ * restores the default ($SDK_PLANE_MRV, built-in 128).  Results never
  * depend on it.  Returns the setting in effect before the call (the
  * default's value when no override was set), -2 for an out-of-range value
  * (nothing changed). */

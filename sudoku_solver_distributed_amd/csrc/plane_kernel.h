@@ -61,9 +61,11 @@
 #define SDK_PLANE_CHUNK 64
 #endif
 // passes on a board before its search switches from the walk's branch order
-// to the completion count (plane::search_step; 0: never)
+// to the completion count (plane::search_step; 0: never).  128 since round 6
+// (box -> row pointing on): the metric's boards are unchanged, the
+// search-heavy set +6 %, an 8-GPU rank +3 % against 64
 #ifndef SDK_PLANE_MRV
-#define SDK_PLANE_MRV 64
+#define SDK_PLANE_MRV 128
 #endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1

@@ -136,17 +136,17 @@ def test_plane_tuning_rejects_oversized_chunks():
 
 def test_plane_search_knob_range():
     """sdk_set_plane_search: the setting in effect before the call back (the
-    default's value, 64, when nothing overrode it), out-of-range values
+    default's value, 128, when nothing overrode it), out-of-range values
     refused with -2 and nothing changed.  Host-side only."""
     from sudoku_solver_distributed_amd import _lib
     L = _lib.load()
     try:
         L.sdk_set_plane_search(-1)
-        assert L.sdk_set_plane_search(48) == 64
+        assert L.sdk_set_plane_search(48) == 128
         assert L.sdk_set_plane_search(0) == 48
         assert L.sdk_set_plane_search(1 << 24) == -2
         assert L.sdk_set_plane_search(-1) == 0
-        assert L.sdk_set_plane_search(-1) == 64
+        assert L.sdk_set_plane_search(-1) == 128
     finally:
         L.sdk_set_plane_search(-1)
 

@@ -141,7 +141,7 @@ def test_search_mode_switch_same_results(solver, order):
     p[11, 5] = 13
     p[40_000] = torch.tensor(b81(CLASH), dtype=torch.uint8)
     try:
-        assert lib.sdk_set_plane_search(0) == 64  # the default in effect before
+        assert lib.sdk_set_plane_search(0) == 128  # the default in effect before
         want = [t.clone() for t in solver.solve(p, order=order)]
         torch.cuda.synchronize()
         # the generated boards (many completions) against the literal walk
