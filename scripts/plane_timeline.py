@@ -37,7 +37,7 @@ if pd[0] or pd[1]:
     print(f"tail pool: {pd[0]} claims, {pd[1]} failed claims, {pd[2]} flag polls; kcycles claiming {pd[3] / 1e3:.0f}, waiting {pd[4] / 1e3:.0f}, solving {pd[5] / 1e3:.0f}")
 cap = 1 << 20
 total = int(lib.sdk_workspace_bytes())
-pool_bytes = 8 * (64 + 16384 * 37 + 1024 * 64) * 4  # PLANE_POOL_BYTES (common.h), after the deferred list
+pool_bytes = 8 * (32 + 16384 * 37) * 4  # PLANE_POOL_BYTES (common.h, round 6 layout), after the deferred list
 list_off = total - pool_bytes - cap * 8
 waves = (min(n, 256 * 4 * 64 * (gw or 4))) // 64
 st = ws[list_off + (cap // 2) * 8: list_off + (cap // 2) * 8 + waves * 256].view(torch.int64).cpu().numpy().reshape(-1, 32)

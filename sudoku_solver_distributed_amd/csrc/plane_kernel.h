@@ -67,6 +67,11 @@
 #ifndef SDK_PLANE_MRV
 #define SDK_PLANE_MRV 128
 #endif
+// guided claims: a wave takes (boards left, as of its own last claim) /
+// (SDK_PLANE_GUIDE x waves), at least its idle lanes, at most `chunk`
+#ifndef SDK_PLANE_GUIDE
+#define SDK_PLANE_GUIDE 2
+#endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
 #endif
@@ -1013,7 +1018,8 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
                     // the head (an agent-scope load of it, or a per-XCD hint
                     // in L2) measured slower: more claims, each a span DMA and
                     // a conversion, and all waves then drain at once
-                    int64_t c = chunk > 0 ? (n - (res_hi > nt ? res_hi : nt)) / (2 * nwaves) : 0;
+                    const int64_t seen = res_hi > nt ? res_hi : nt;
+                    int64_t c = chunk > 0 ? (n - seen) / (SDK_PLANE_GUIDE * nwaves) : 0;
                     c = c > chunk ? chunk : c;
                     // a chunk is staged and converted in one go: at most 64 records
                     // fit the staging area (the host also rejects chunk > 64)
