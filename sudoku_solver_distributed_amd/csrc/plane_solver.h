@@ -238,14 +238,15 @@ PS_FN uint32_t fold_rows(uint32_t y) { return (y | (y >> 10) | (y >> 20)) & 0x1F
 struct Board;
 PS_FN void pin_board(Board &B);
 
-// One propagation pass (rules A, B, C above).  Returns DEAD, SOLVED, STUCK
-// (a fixpoint: und[] = the undetermined cells, each with >= 2 candidates) or
-// OPEN (something changed: pass again).
+// One propagation pass (rules A-D above).  Returns DEAD, SOLVED, STUCK (no
+// single found: und[] = the undetermined cells; rule D may still have
+// removed places, which the next pass sees) or OPEN (pass again).
 //
 // Written for the full-rate issue forms (see or3() above): two-input ops
 // with literal constants, three-input logic as v_bitop3_b32 on VGPRs, right
-// shifts only, and one v_mul_u32_u24 per spread of a 9-bit set over three
-// rows.  ~1380 issue slots per pass (profiles/isa_plane_pass.json).
+// shifts only, 16-bit multiplies for 9-bit results, and one v_mul_u32_u24
+// per spread of a set over a band's three rows.  1824 VALU per pass with
+// SDK_PLANE_LC 3 (profiles/isa_plane_pass.json).
 PS_FN int pass(Board &B, uint32_t und[3])
 {
     uint32_t single[3], nd[3];
