@@ -70,7 +70,7 @@
 // guided claims: a wave takes (boards left, as of its own last claim) /
 // (SDK_PLANE_GUIDE x waves), at least its idle lanes, at most `chunk`
 #ifndef SDK_PLANE_GUIDE
-#define SDK_PLANE_GUIDE 2
+#define SDK_PLANE_GUIDE 3
 #endif
 #ifndef SDK_PLANE_PUSH_PAD
 #define SDK_PLANE_PUSH_PAD 1
@@ -854,7 +854,7 @@ __device__ __forceinline__ void plane_body(const IO &io, unsigned long long *__r
     // wave claims a CHUNK of boards at a time into its reservoir [res_lo,
     // res_hi) and refills from it: one queue atomic per chunk instead of per
     // refill (the head is one device-scope atomic for 4096 waves).  Chunks
-    // shrink towards the end of the batch (guided: remaining / (2 waves)).
+    // shrink towards the end of the batch (guided: remaining / (SDK_PLANE_GUIDE waves)).
     int64_t res_lo = 0, res_hi = 0;
     int64_t rec_base = 0;  // virtual index of chunk record 0
     int64_t rec_id = 0;    // its board id
