@@ -204,7 +204,7 @@ PS_FN uint32_t box_cols(uint32_t c)
 // rule D, box -> row, on one band word y of a digit's plane: the cells to
 // clear because a box of the band holds all its places in one row -- that
 // row outside the box.  (Two boxes pointing into two rows: each one's cells
-// in the other's row hold no place already.)  17 VALU, applied.
+// in the other's row hold no place already.)  16 VALU, applied.
 // point_rows_parts: the rows to clear and the pointing boxes' area (clear =
 // rows outside the area); point_rows(y) = the cells to clear; point_rows_apply
 // clears them from y in one v_bitop3.
@@ -213,9 +213,9 @@ PS_FN void point_rows_parts(uint32_t y, uint32_t &rows, uint32_t &area)
     const uint32_t r3 = or3(y, y >> 1, y >> 2) & 0x4912449u;  // row k of box j has a place: bit 10k + 3j
     const uint32_t a1 = r3 >> 10, a2 = r3 >> 20;
     const uint32_t hbox = box_one(xor3(r3, a1, a2), maj3(r3, a1, a2));  // boxes with places in one row
-    const uint32_t rn = ((r3 & mul24(hbox, 0x100401u)) + ROWS) & GUARDS;   // the rows of those segments
-    rows = rn - (rn >> 9);
     area = mul24(hbox, 0x701C07u);
+    const uint32_t rn = ((r3 & area) + ROWS) & GUARDS;  // the rows of those boxes' places (r3 holds bits 10k + 3j only)
+    rows = rn - (rn >> 9);
 }
 PS_FN uint32_t point_rows(uint32_t y)
 {
