@@ -245,7 +245,7 @@ PS_FN void pin_board(Board &B);
 // Written for the full-rate issue forms (see or3() above): two-input ops
 // with literal constants, three-input logic as v_bitop3_b32 on VGPRs, right
 // shifts only, 16-bit multiplies for 9-bit results, and one v_mul_u32_u24
-// per spread of a set over a band's three rows.  1824 VALU per pass with
+// per spread of a set over a band's three rows.  1797 VALU per pass with
 // SDK_PLANE_LC 3 (profiles/isa_plane_pass.json).
 PS_FN int pass(Board &B, uint32_t und[3])
 {
