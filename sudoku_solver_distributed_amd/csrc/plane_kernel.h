@@ -46,9 +46,12 @@
 #define SDK_PLANE_TAIL 6  // 12 until rule D and the open-root count shortened the heavy boards
 #endif
 // 2: continue through the XCD's tail pool on the wave-wide solver, 1: the
-// wave-wide solver on the wave's own boards only
+// wave-wide solver on the wave's own boards only.  1 since round 6: with
+// ~15 passes per board a wave's last boards end soon enough that sharing
+// them through the pool (claims, flags) costs more than it evens out
+// (+2.7 % on an 8-GPU rank, +1 % on a 4-GPU one, +2 % search-heavy)
 #ifndef SDK_PLANE_TAIL_MODE
-#define SDK_PLANE_TAIL_MODE 2
+#define SDK_PLANE_TAIL_MODE 1
 #endif
 // a pipelined launch's (SDK_GRID_PIPELINED)
 #ifndef SDK_PLANE_PIPE_TAIL

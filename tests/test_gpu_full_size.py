@@ -111,6 +111,7 @@ def test_bench_rank_shape_vs_oracle(solver, full_batch):
 
 _TIMEOUT_CHILD = r"""
 import os, sys
+os.environ["SDK_PLANE_TAIL_MODE"] = "2"     # the XCD pool (tail mode 1 is the default)
 sys.path.insert(0, sys.argv[1])
 import numpy as np, torch
 from sudoku_solver_distributed_amd.gen import hard17_batch
