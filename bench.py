@@ -510,7 +510,8 @@ def main():
     shard = hi - lo  # this rank's boards per step
     if shard <= 0:
         raise SystemExit("--batch too small for the number of ranks")
-    # steps per launch: enough consecutive steps' shards to fill a launch.
+    # steps per launch: enough consecutive steps' shards to fill a launch
+    # (--plan inflight; the default plan "run" sets the group below).
     # Sharded steps (N > 1) go 2^21 boards to a launch at 2 waves per SIMD:
     # fewer launches, so fewer drains at the end of the run (one rank of
     # N = 2 / 4 / 8 at 20 steps: +6 / +6 / +5 % over 2^20 at 1 wave)
