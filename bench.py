@@ -408,8 +408,11 @@ def side_configs(solver, dev, world, rank, boards, serving: bool = True):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=2)
+    # the driver's own K / W (BENCH_r05's command): a run with no flags is the
+    # launch shape profiles/pmc_plane_kernel_multi_w1.json was counted on, so
+    # its line carries roofline.frac too
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=1 << 20,
                     help="boards per step: over all GPUs (--scaling strong) or per GPU (weak)")
     ap.add_argument("--scaling", choices=("strong", "weak"), default="strong",
